@@ -1,0 +1,250 @@
+"""Benchmark: GD inner-loop iterations/s for a batch of trajectories.
+
+BASELINE.json metric "GD iterations/sec (batch of trajectories) at 1/2/4/8
+MI355X; % HBM roofline", workload configs[2] (C3): per GPU a batch of 1024
+random start/goal problems, N=128 waypoints, D=3 joints, the reference's 11
+obstacles shared by the batch, GradientDescentOptimizer.  One step = one
+optimize() of the whole batch (initTrajectory + the full inner loop) in one
+persistent launch, inputs resident in HBM.  Bench mode runs every trajectory
+for exactly --max-inner (200) iterations (loop_loss_reduction = -1e30,
+max_outer_iteration = 1), so iterations/s = B·200/t.
+
+Multi-GPU (torchrun, one rank per GPU): weak scaling, each rank owns a
+1024-problem shard; the shared environment is broadcast from rank 0 over
+RCCL (the only collective besides the timing/iteration reductions).
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+CONFIGS = {
+    # name: (description, B per GPU, N, D, O, optimizer)
+    "c3": ("batch of 1024 random start/goal trajectories, N=128, D=3, 11 shared obstacles, GD (BASELINE configs[2])",
+           1024, 128, 3, 11, "gd"),
+    "c4": ("batch of 1024 per GPU (8192 on 8), N=256, D=3, 50 random obstacles, GD (BASELINE configs[3])",
+           1024, 256, 3, 50, "gd"),
+    "c5": ("7-DoF arm, batch of 512 per GPU (4096 on 8), N=256, 11 obstacles, GD (BASELINE configs[4])",
+           512, 256, 7, 11, "gd"),
+    "c2": ("single trajectory, N=128, 10 obstacles, BLS (BASELINE configs[1])", 1, 128, 3, 10, "bls"),
+}
+
+PEAK_FP32_TFLOPS = 157.3  # MI355X fp32 (vector = matrix), MI355X_MICROARCH.md
+PEAK_HBM_GBS = 8000.0
+
+
+def make_problem(cfg, world, rank):
+    """Synthetic inputs of SURVEY.md §8d (numpy default_rng), this rank's shard."""
+    _, B, N, D, O, _ = CONFIGS[cfg]
+    Btot = B * world
+    if cfg == "c4":
+        rng = np.random.default_rng(2)
+        obs = []
+        while len(obs) < O:
+            o = rng.uniform(-3.5, 3.5, 2)
+            if np.linalg.norm(o) >= 0.5:
+                obs.append(o)
+        obstacles = np.array(obs, np.float32)
+        rs = np.random.default_rng(3)
+    else:
+        from irm_motion_planning_amd.environment import OBSTACLES
+        obstacles = OBSTACLES[:O].astype(np.float32)
+        rs = np.random.default_rng(4 if cfg == "c5" else 1)
+    start = rs.uniform(-0.5, 0.5, (Btot, D)).astype(np.float32)
+    goal = rs.uniform(0.2, 1.6, (Btot, D)).astype(np.float32)
+    if cfg == "c2":
+        from irm_motion_planning_amd.environment import START_CONFIG, GOAL_CONFIG
+        start[:] = START_CONFIG
+        goal[:] = GOAL_CONFIG
+    sl = slice(rank * B, (rank + 1) * B)
+    return start[sl], goal[sl], obstacles
+
+
+def make_args(cfg, faithful, max_inner):
+    from irm_motion_planning_amd import main as irm_main
+    _, B, N, D, O, opt = CONFIGS[cfg]
+    argv = ["--optimizer-name", opt, "--n-timesteps", str(N), "--n-joints", str(D)]
+    if D != 3:
+        argv += ["--link-length"] + [str(3.0 / D)] * D
+    if not faithful:
+        argv += ["--loop-loss-reduction=-1e30", "--max-outer-iteration=1", f"--max-inner-iteration={max_inner}"]
+    return irm_main.parse_args(argv)
+
+
+def flops_per_iteration(N, D, O, R):
+    """Algorithmic fp32 flops of one GD iteration of one trajectory.
+
+    exec: what the trajectory-space rank-R kernel must do — stage 1 (Fᵀa,
+    2·R·N·D), stage 2 (F·y, 2·2N·R·D), the JᵀJ mix (2·R·D²), the update
+    (4·N·D), obstacle pairs (14·N·O), FK/Jacobian/penalties (24·N·D, sincos
+    counted as 4 flops each).
+    ref: SURVEY.md §8d's count of the reference formulation, 12N²D + 10ND² + 22NO.
+    """
+    exec_f = 2 * R * N * D + 4 * N * R * D + 2 * R * D * D + 4 * N * D + 14 * N * O + 24 * N * D
+    ref_f = 12 * N * N * D + 10 * N * D * D + 22 * N * O
+    return exec_f, ref_f
+
+
+def cpu_baseline(cfg, args, start, goal, obstacles, budget_s=12.0):
+    """Oracle (C restatement of the reference, OpenMP over trajectories) on a bounded sample."""
+    from irm_motion_planning_amd.params import params_from_args
+    from oracle.oracle import Oracle
+    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    p = params_from_args(args)
+    orc = Oracle(p)
+    t0 = time.perf_counter()
+    _, st1 = orc.optimize_batch(None, start[:1], goal[:1], obstacles, n_threads=1)
+    t1 = time.perf_counter() - t0
+    n = int(max(cores, min(len(start), budget_s / max(t1, 1e-6) * cores)))
+    n = max(cores, (n // cores) * cores)
+    n = min(n, len(start))
+    t0 = time.perf_counter()
+    _, st = orc.optimize_batch(None, start[:n], goal[:n], obstacles, n_threads=cores)
+    dt = time.perf_counter() - t0
+    iters = sum(s["grad_evals"] for s in st)
+    return {"value": iters / dt, "unit": "GD iterations/s", "cores": cores, "kind": "port",
+            "sample": f"{n} of the {len(start)} rank-0 problems, full optimize() each ({iters} iterations, "
+                      f"{dt:.2f} s wall on {cores} threads); 1-thread rate {st1[0]['grad_evals'] / t1:.1f} it/s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--faithful", action="store_true", help="reference control flow (early exits) instead of 200 fixed")
+    ap.add_argument("--max-inner", type=int, default=200)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--operator-rank", type=int, default=0)
+    ap.add_argument("--tb", type=int, default=0, help="trajectories per workgroup (0 = auto)")
+    a = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from irm_motion_planning_amd.context import Context, batch_dev
+    from irm_motion_planning_amd._abi import IrmStats
+    from irm_motion_planning_amd.params import params_from_args
+
+    desc, B, N, D, O, opt = CONFIGS[a.config]
+    args = make_args(a.config, a.faithful, a.max_inner)
+    start, goal, obstacles = make_problem(a.config, world, rank)
+
+    # shared environment: rank 0's obstacles broadcast over RCCL/xGMI
+    obs_t = torch.from_numpy(obstacles).to(dev)
+    if world > 1:
+        dist.broadcast(obs_t, src=0)
+    start_t = torch.from_numpy(start).to(dev)
+    goal_t = torch.from_numpy(goal).to(dev)
+    alpha_t = torch.empty((B, N, D), dtype=torch.float32, device=dev)
+    traj_t = torch.empty_like(alpha_t)
+    stats_t = torch.zeros((B, 8), dtype=torch.int32, device=dev)  # irm_stats = 8 × 4 bytes
+
+    ctx = Context(params_from_args(args, operator_rank=a.operator_rank, device=local, traj_per_block=a.tb))
+    info = ctx.info()
+    bd = batch_dev(start=start_t.data_ptr(), goal=goal_t.data_ptr(), obstacles=obs_t.data_ptr(), n_obstacles=O,
+                   batch=B, alpha_out=alpha_t.data_ptr(), traj_out=traj_t.data_ptr(), stats_out=stats_t.data_ptr())
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        ctx.optimize_dev(bd, stream.cuda_stream)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(stream)
+        step()
+        e1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+
+    st = stats_t.cpu().numpy()
+    iters_rank = float(st[:, 2].sum())  # grad_evals = executed inner iterations
+    t_tensor = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    it_tensor = torch.tensor([iters_rank], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t_tensor, op=dist.ReduceOp.MAX)
+        dist.all_reduce(it_tensor, op=dist.ReduceOp.SUM)
+    elapsed_max = float(t_tensor.item())
+    iters_all = float(it_tensor.item())
+    value = iters_all * a.steps / elapsed_max
+
+    exec_f, ref_f = flops_per_iteration(N, D, O, info["operator_rank"])
+    launch_flops = exec_f * iters_rank
+    achieved = launch_flops / (kernel_ms * 1e-3) / 1e12
+    bytes_launch = B * (2 * D + 2 * N * D) * 4 + B * 32  # start/goal in; alpha/traj/stats out
+    result = {
+        "metric": "GD iterations/sec (batch of trajectories)",
+        "value": value,
+        "unit": "iterations/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": 1000 * elapsed_max / a.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (SURVEY.md §8d seeds), reference environment",
+        "config": {
+            "workload": f"{a.config}: {desc}",
+            "batch_per_gpu": B, "global_batch": B * world, "n_timesteps": N, "n_joints": D, "n_obstacles": O,
+            "optimizer": opt, "mode": "faithful" if a.faithful else f"bench ({a.max_inner} fixed GD iterations)",
+            "operator_rank": info["operator_rank"], "traj_per_block": info["traj_per_block"],
+            "parallelism": f"dp{world} (batch sharded, env broadcast over RCCL)",
+        },
+        "roofline": {
+            "bound": "mfma",
+            "achieved": achieved,
+            "peak": PEAK_FP32_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved / PEAK_FP32_TFLOPS,
+            "traffic": None,
+            "kernel": "irm::k_optimize (fp32 MFMA 16x16x4 + VALU)",
+            "kernel_ms": kernel_ms,
+            "flops_per_iteration": exec_f,
+            "ref_formulation_flops_per_iteration": ref_f,
+            "ref_formulation_tflops": ref_f * iters_rank / (kernel_ms * 1e-3) / 1e12,
+            "hbm_algorithmic_bytes_per_launch": bytes_launch,
+            "hbm_frac": bytes_launch / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+        },
+        "cpu_baseline": None,
+        "iterations_per_step": iters_all,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(a.config, args, start, goal, obstacles)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,907 @@
+// irm_host.cpp — C ABI (include/irm.h) of the MI355X trajectory optimiser.
+//
+// Context creation builds, once per configuration, everything
+// Trajectory.__init__ builds (trajectory.py:23-42) plus the device-side
+// operators of the trajectory-space formulation:
+//   L = [K; dK]                (2N × N, fp32 exactly as the reference)
+//   F = L·V_R                  (V_R: top-R eigenvectors of LᵀL, fp64 Jacobi)
+// packed into the 16x16x4 MFMA A-fragment layout and uploaded to HBM.
+// All per-call numerics run in irm_kernels.hip; there is no CPU fallback.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/irm.h"
+#include "irm_kernels.hpp"
+
+using irm::KParams;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess) return fail(IRM_EKERNEL, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+// ------------------------------------------------------------- host linalg
+// Cyclic Jacobi eigen-decomposition of a symmetric n×n matrix (fp64).
+// On return a's diagonal holds the eigenvalues and v the eigenvectors (columns).
+void jacobi_eigen(std::vector<double>& a, int n, std::vector<double>& v) {
+    v.assign((size_t)n * n, 0.0);
+    for (int i = 0; i < n; ++i) v[(size_t)i * n + i] = 1.0;
+    double fro = 0.0;
+    for (double x : a) fro += x * x;
+    fro = sqrt(fro);
+    for (int sweep = 0; sweep < 64; ++sweep) {
+        double off = 0.0;
+        for (int p = 0; p < n; ++p)
+            for (int q = p + 1; q < n; ++q) off += a[(size_t)p * n + q] * a[(size_t)p * n + q];
+        if (sqrt(off) <= 1e-17 * fro) break;
+        for (int p = 0; p < n; ++p) {
+            for (int q = p + 1; q < n; ++q) {
+                double apq = a[(size_t)p * n + q];
+                if (fabs(apq) <= 1e-300) continue;
+                double app = a[(size_t)p * n + p], aqq = a[(size_t)q * n + q];
+                double theta = (aqq - app) / (2.0 * apq);
+                double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < n; ++k) {  // rotate columns p, q
+                    double akp = a[(size_t)k * n + p], akq = a[(size_t)k * n + q];
+                    a[(size_t)k * n + p] = c * akp - s * akq;
+                    a[(size_t)k * n + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < n; ++k) {  // rotate rows p, q
+                    double apk = a[(size_t)p * n + k], aqk = a[(size_t)q * n + k];
+                    a[(size_t)p * n + k] = c * apk - s * aqk;
+                    a[(size_t)q * n + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < n; ++k) {
+                    double vkp = v[(size_t)k * n + p], vkq = v[(size_t)k * n + q];
+                    v[(size_t)k * n + p] = c * vkp - s * vkq;
+                    v[(size_t)k * n + q] = s * vkp + c * vkq;
+                }
+            }
+        }
+    }
+}
+
+// fp32 LU with partial pivoting; solves A·X = B (n×n, nrhs columns, row-major).
+// fp32 on purpose: trajectory.py:77 solves the singular K in fp32 (|α|≈1e3).
+bool lu_solve_f32(int n, const float* A_in, const float* B_in, int nrhs, float* X) {
+    std::vector<float> A(A_in, A_in + (size_t)n * n), B(B_in, B_in + (size_t)n * nrhs);
+    for (int k = 0; k < n; ++k) {
+        int p = k;
+        for (int i = k + 1; i < n; ++i)
+            if (fabsf(A[(size_t)i * n + k]) > fabsf(A[(size_t)p * n + k])) p = i;
+        if (A[(size_t)p * n + k] == 0.f) return false;
+        if (p != k) {
+            for (int j = 0; j < n; ++j) std::swap(A[(size_t)k * n + j], A[(size_t)p * n + j]);
+            for (int j = 0; j < nrhs; ++j) std::swap(B[(size_t)k * nrhs + j], B[(size_t)p * nrhs + j]);
+        }
+        const float piv = A[(size_t)k * n + k];
+        for (int i = k + 1; i < n; ++i) {
+            const float l = A[(size_t)i * n + k] / piv;
+            A[(size_t)i * n + k] = l;
+            for (int j = k + 1; j < n; ++j) A[(size_t)i * n + j] -= l * A[(size_t)k * n + j];
+            for (int j = 0; j < nrhs; ++j) B[(size_t)i * nrhs + j] -= l * B[(size_t)k * nrhs + j];
+        }
+    }
+    for (int j = 0; j < nrhs; ++j)
+        for (int i = n - 1; i >= 0; --i) {
+            float s = B[(size_t)i * nrhs + j];
+            for (int k = i + 1; k < n; ++k) s -= A[(size_t)i * n + k] * X[(size_t)k * nrhs + j];
+            X[(size_t)i * nrhs + j] = s / A[(size_t)i * n + i];
+        }
+    return true;
+}
+
+// ------------------------------------------------ legacy threefry (J)
+uint32_t rotl32(uint32_t v, int r) { return (v << r) | (v >> (32 - r)); }
+
+void threefry2x32(uint32_t k0, uint32_t k1, uint32_t& x0, uint32_t& x1) {
+    static const int rot[2][4] = {{13, 15, 26, 6}, {17, 29, 16, 24}};
+    static const int inj[5][2] = {{1, 2}, {2, 0}, {0, 1}, {1, 2}, {2, 0}};
+    const uint32_t ks[3] = {k0, k1, k0 ^ k1 ^ 0x1BD11BDAu};
+    uint32_t a = x0 + ks[0], b = x1 + ks[1];
+    for (int i = 0; i < 5; ++i) {
+        for (int r = 0; r < 4; ++r) {
+            a += b;
+            b = rotl32(b, rot[i % 2][r]);
+            b ^= a;
+        }
+        a += ks[inj[i][0]];
+        b += ks[inj[i][1]] + (uint32_t)(i + 1);
+    }
+    x0 = a;
+    x1 = b;
+}
+
+double erfinv_f64(double y) {
+    if (y <= -1.0) return -INFINITY;
+    if (y >= 1.0) return INFINITY;
+    const double a = 0.147, ln = log(1.0 - y * y);
+    const double t1 = 2.0 / (M_PI * a) + ln / 2.0;
+    double x = copysign(sqrt(sqrt(t1 * t1 - ln / a) - t1), y);
+    for (int it = 0; it < 60; ++it) {  // Newton on erf(x) = y
+        const double step = (erf(x) - y) / (2.0 / sqrt(M_PI) * exp(-x * x));
+        x -= step;
+        if (fabs(step) < 1e-17 * (1.0 + fabs(x))) break;
+    }
+    return x;
+}
+
+void fill_frag(std::vector<float>& out, int M, int K, const std::vector<double>& A /*row-major M×K*/) {
+    out.assign((size_t)irm::frag_floats(M, K), 0.f);
+    for (int r = 0; r < M; ++r)
+        for (int k = 0; k < K; ++k) out[(size_t)irm::frag_index(r, k, K)] = (float)A[(size_t)r * K + k];
+}
+
+int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+// ================================================================ context
+struct irm_ctx {
+    irm_params p{};
+    int N = 0, D = 0, R = 0, NK = 0, MP = 0, RP = 0;
+    float trunc = 0.f;
+    std::vector<float> t, cvec, K, dK, J;
+    KParams kp{};
+    // device
+    float *d_Lfrag = nullptr, *d_LTfrag = nullptr, *d_F1 = nullptr, *d_F2 = nullptr, *d_Fbot = nullptr,
+          *d_Vr = nullptr, *d_Vfrag = nullptr, *d_u = nullptr, *d_w = nullptr;
+    // host-API staging
+    void* d_io = nullptr;
+    size_t io_bytes = 0;
+    hipStream_t stream = nullptr;
+    int num_cus = 0;
+    char name[64] = {0}, arch[32] = {0};
+    int tb_opt = 1, ops_lds = 0, lds_opt = 0;
+    int max_series = 0;
+    unsigned long long* d_prof = nullptr;  // IRM_PHASE_PROFILE builds only
+    int prof_blocks = 0, prof_cap = 0;
+};
+
+namespace {
+
+int ensure_io(irm_ctx* c, size_t bytes) {
+    if (bytes <= c->io_bytes) return 0;
+    if (c->d_io) (void)hipFree(c->d_io);
+    c->d_io = nullptr;
+    c->io_bytes = 0;
+    bytes = std::max<size_t>(bytes, 1 << 20);
+    HIP_TRY(hipMalloc(&c->d_io, bytes));
+    c->io_bytes = bytes;
+    return 0;
+}
+
+int upload(float** dst, const std::vector<float>& src) {
+    HIP_TRY(hipMalloc(dst, std::max<size_t>(src.size(), 4) * sizeof(float)));
+    if (!src.empty()) HIP_TRY(hipMemcpy(*dst, src.data(), src.size() * sizeof(float), hipMemcpyHostToDevice));
+    return 0;
+}
+
+// Workgroup shape for a launch of B trajectories: one lane per (trajectory,
+// waypoint), NW = N rounded up to 64 lanes per trajectory, TB trajectories
+// per workgroup with TB·D ≤ 16 MFMA columns and TB·NW ≤ 1024 threads.  For
+// the optimiser TB defaults to ⌈B / #CU⌉ (one workgroup per CU when B is
+// small) and the operator fragments are staged into LDS when they fit.
+int choose_shape(const irm_ctx* c, int B, bool optimizer, KParams& kp, int* lds_bytes_out) {
+    const int D = c->D;
+    kp.NW = round_up(c->N, 64);
+    // D ≥ 5 needs > 128 VGPRs per lane: keep those workgroups at ≤ 512 threads
+    const int maxthreads = (D >= 5) ? 512 : irm::kMaxThreads;
+    const int tbmax = std::max(1, std::min(irm::kCols / D, maxthreads / kp.NW));
+    int tb = tbmax;
+    if (optimizer && c->p.traj_per_block > 0) tb = std::min(c->p.traj_per_block, tbmax);
+    else if (optimizer) tb = std::min(tbmax, std::max(1, (B + c->num_cus - 1) / std::max(1, c->num_cus)));
+    tb = std::max(1, std::min(tb, std::max(1, B)));
+    const size_t lds_cap = 160 * 1024;
+    for (; tb >= 1; --tb) {
+        kp.TB = tb;
+        kp.BT = tb * kp.NW;
+        const int nw = kp.BT / 64, MT1 = kp.RP / 16, KQ1 = kp.NK / 16;
+        kp.nsplit = std::max(1, std::min(KQ1, nw / std::max(1, MT1)));
+        if (optimizer) {
+            irm::Plan a = irm::plan_lds(kp, true, true);
+            if ((size_t)a.total * 4 <= lds_cap) {
+                kp.ops_in_lds = 1;
+                if (lds_bytes_out) *lds_bytes_out = a.total * 4;
+                return tb;
+            }
+            irm::Plan b = irm::plan_lds(kp, false, true);
+            if ((size_t)b.total * 4 <= lds_cap) {
+                kp.ops_in_lds = 0;
+                if (lds_bytes_out) *lds_bytes_out = b.total * 4;
+                return tb;
+            }
+        } else {
+            irm::Plan a = irm::plan_lds(kp, false, false);
+            if ((size_t)a.total * 4 <= lds_cap) {
+                if (lds_bytes_out) *lds_bytes_out = a.total * 4;
+                return tb;
+            }
+        }
+    }
+    return 0;
+}
+
+int set_device(const irm_ctx* c) {
+    HIP_TRY(hipSetDevice(c->p.device));
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+void irm_params_default(irm_params* p) {
+    memset(p, 0, sizeof(*p));
+    p->n_timesteps = 50;
+    p->n_joints = 3;
+    p->optimizer = IRM_OPT_BLS;
+    p->max_inner_iteration = 200;
+    p->max_outer_iteration = 10;
+    p->max_bls_iteration = 20;
+    p->constraint_violating_dependant_loss = 1;
+    const float lr[10] = {2e-3f, 1e-4f, 1e-5f, 1e-6f, 1e-7f, 1e-8f, 1e-8f, 1e-8f, 1e-8f, 1e-8f};
+    p->n_gd_lr = 10;
+    for (int i = 0; i < 10; ++i) p->gd_lr[i] = lr[i];
+    p->rbf_variance = 0.1f;
+    p->loop_loss_reduction = 1e-3f;
+    p->lambda_constraint_increase = 10.f;
+    p->lambda_sg_constraint = 0.5f;
+    p->lambda_jl_constraint = 0.1f;
+    p->eps_position = 0.01f;
+    p->eps_velocity = 0.01f;
+    p->lambda_max_cost = 0.5f;
+    p->lambda_reg = 1e-4f;
+    p->joint_safety_limit = 0.98f;
+    p->bls_lr_start = 0.2f;
+    p->bls_alpha = 0.01f;
+    p->bls_beta_plus = 1.2f;
+    p->bls_beta_minus = 0.5f;
+    p->max_joint_velocity = 7.f;
+    p->max_joint_position = 2.f;
+    p->min_joint_position = -1.f;
+    p->link_length[0] = 1.5f;
+    p->link_length[1] = 1.0f;
+    p->link_length[2] = 0.5f;
+    irm_default_jac(3, 0.15f, 0u, p->jac);
+    p->operator_rank = 0;
+    p->operator_tol = 1e-12f;
+    p->device = 0;
+}
+
+int irm_default_jac(int32_t D, float jgm, uint32_t seed, float* jac_out) {
+    if (D < 1 || D > IRM_MAX_JOINTS || !jac_out) return fail(IRM_EINVAL, "irm_default_jac: bad arguments");
+    const int n = D * D, odd = n & 1, half = (n + odd) / 2;
+    std::vector<uint32_t> cnt(2 * half, 0u), bits(2 * half, 0u);
+    for (int i = 0; i < n; ++i) cnt[i] = (uint32_t)i;
+    for (int i = 0; i < half; ++i) {
+        uint32_t x0 = cnt[i], x1 = cnt[half + i];
+        threefry2x32(0u, seed, x0, x1);  // PRNGKey(seed) = [0, seed]
+        bits[i] = x0;
+        bits[half + i] = x1;
+    }
+    const float lo = nextafterf(-1.f, 0.f);
+    for (int i = 0; i < n; ++i) {
+        uint32_t fb = (bits[i] >> 9) | 0x3F800000u;
+        float f;
+        memcpy(&f, &fb, 4);
+        f -= 1.f;
+        float u = std::max(lo, f * (1.f - lo) + lo);
+        float z = (float)sqrt(2.0) * (float)erfinv_f64((double)u);
+        jac_out[i] = ((i / D) == (i % D) ? 1.f : 0.f) + jgm * z;
+    }
+    return IRM_OK;
+}
+
+const char* irm_last_error(void) { return g_err.c_str(); }
+
+int irm_ctx_create(irm_ctx** out, const irm_params* p) {
+    if (!out || !p) return fail(IRM_EINVAL, "irm_ctx_create: null argument");
+    *out = nullptr;
+    const int N = p->n_timesteps, D = p->n_joints;
+    if (N < 2 || N > IRM_MAX_TIMESTEPS) return fail(IRM_EINVAL, "n_timesteps=%d outside [2, %d]", N, IRM_MAX_TIMESTEPS);
+    if (D < 1 || D > IRM_MAX_JOINTS) return fail(IRM_EINVAL, "n_joints=%d outside [1, %d]", D, IRM_MAX_JOINTS);
+    if (p->optimizer != IRM_OPT_GD && p->optimizer != IRM_OPT_BLS) return fail(IRM_EINVAL, "unknown optimizer %d", p->optimizer);
+    if (p->optimizer == IRM_OPT_GD && p->max_outer_iteration > p->n_gd_lr)
+        return fail(IRM_EINVAL, "max_outer_iteration and dual_lr do not match");  // optimizer_GD.py:34-36
+    if (p->n_gd_lr > IRM_MAX_LR) return fail(IRM_EINVAL, "at most %d --gd-lr entries", IRM_MAX_LR);
+    if (p->max_bls_iteration < 1 && p->optimizer == IRM_OPT_BLS) return fail(IRM_EINVAL, "max_bls_iteration must be >= 1");
+    if (!(p->rbf_variance > 0.f)) return fail(IRM_EINVAL, "rbf_variance must be > 0");
+
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= p->device || p->device < 0)
+        return fail(IRM_EDEVICE, "no HIP device %d (found %d): this library has no CPU fallback", p->device, ndev);
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, p->device));
+    if (!strstr(prop.gcnArchName, "gfx950"))
+        return fail(IRM_EDEVICE, "device %d is %s; this build targets gfx950 (MI355X) only", p->device, prop.gcnArchName);
+    HIP_TRY(hipSetDevice(p->device));
+
+    irm_ctx* c = new irm_ctx();
+    c->p = *p;
+    c->N = N;
+    c->D = D;
+    c->num_cus = prop.multiProcessorCount;
+    snprintf(c->name, sizeof(c->name), "%s", prop.name);
+    snprintf(c->arch, sizeof(c->arch), "%s", prop.gcnArchName);
+
+    // ---- Trajectory.__init__ (trajectory.py:31-42), fp32 as the reference
+    c->t.resize(N);
+    c->cvec.resize(N);
+    {
+        const float div = (float)(N - 1);
+        for (int i = 0; i < N - 1; ++i) {
+            const float st = (float)i / div;
+            c->t[i] = 0.f * (1.f - st) + 1.f * st;
+        }
+        c->t[N - 1] = 1.f;
+        for (int i = 0; i < N; ++i) {
+            const float tt = c->t[i], t3 = tt * tt * tt, t4 = t3 * tt, t5 = t4 * tt;
+            c->cvec[i] = 6.f * t5 - 15.f * t4 + 10.f * t3;
+        }
+    }
+    c->K.resize((size_t)N * N);
+    c->dK.resize((size_t)N * N);
+    {
+        const double sig = p->rbf_variance;
+        const float two_s2 = (float)(2.0 * sig * sig), s2 = (float)(sig * sig);
+        for (int i = 0; i < N; ++i)
+            for (int j = 0; j < N; ++j) {
+                const float d = c->t[j] - c->t[i];
+                const float e = expf(-(d * d) / two_s2);
+                c->K[(size_t)i * N + j] = e;
+                c->dK[(size_t)i * N + j] = d / s2 * e;
+            }
+    }
+    c->J.assign(p->jac, p->jac + (size_t)D * D);
+
+    // ---- operator factorisation F = L·V_R
+    const int NK = round_up(N, 16), MP = round_up(2 * N, 16);
+    std::vector<double> Ld((size_t)2 * N * N);
+    for (int i = 0; i < N; ++i)
+        for (int j = 0; j < N; ++j) {
+            Ld[(size_t)i * N + j] = c->K[(size_t)i * N + j];
+            Ld[(size_t)(N + i) * N + j] = c->dK[(size_t)i * N + j];
+        }
+    int R = 0, RP = 0;
+    std::vector<double> Vd;  // N × RP
+    if (p->operator_rank < 0) {  // dense: F = L, V = I
+        R = N;
+        RP = NK;
+        Vd.assign((size_t)N * RP, 0.0);
+        for (int i = 0; i < N; ++i) Vd[(size_t)i * RP + i] = 1.0;
+        c->trunc = 0.f;
+    } else {
+        std::vector<double> G((size_t)N * N, 0.0), Vfull;
+        for (int i = 0; i < N; ++i)
+            for (int j = i; j < N; ++j) {
+                double s = 0.0;
+                for (int m = 0; m < 2 * N; ++m) s += Ld[(size_t)m * N + i] * Ld[(size_t)m * N + j];
+                G[(size_t)i * N + j] = G[(size_t)j * N + i] = s;
+            }
+        jacobi_eigen(G, N, Vfull);
+        std::vector<int> order(N);
+        for (int i = 0; i < N; ++i) order[i] = i;
+        std::sort(order.begin(), order.end(),
+                  [&](int a, int b) { return G[(size_t)a * N + a] > G[(size_t)b * N + b]; });
+        const double l0 = G[(size_t)order[0] * N + order[0]];
+        if (p->operator_rank > 0) {
+            R = std::min(p->operator_rank, N);
+        } else {
+            const double tol = p->operator_tol > 0.f ? p->operator_tol : 1e-12;
+            R = N;
+            for (int r = 16; r < N; r += 16) {
+                const double lr = std::max(0.0, G[(size_t)order[r] * N + order[r]]);
+                if (lr / l0 < tol) { R = r; break; }
+            }
+        }
+        RP = round_up(R, 16);
+        c->trunc = (R < N) ? (float)(std::max(0.0, G[(size_t)order[R] * N + order[R]]) / l0) : 0.f;
+        Vd.assign((size_t)N * RP, 0.0);
+        for (int i = 0; i < N; ++i)
+            for (int r = 0; r < R; ++r) Vd[(size_t)i * RP + r] = Vfull[(size_t)i * N + order[r]];
+    }
+    c->R = R;
+    c->RP = RP;
+    c->NK = NK;
+    c->MP = MP;
+    std::vector<double> F((size_t)2 * N * RP, 0.0);  // F = L·V
+    for (int m = 0; m < 2 * N; ++m)
+        for (int r = 0; r < RP; ++r) {
+            double s = 0.0;
+            for (int j = 0; j < N; ++j) s += Ld[(size_t)m * N + j] * Vd[(size_t)j * RP + r];
+            F[(size_t)m * RP + r] = s;
+        }
+
+    // fragments
+    std::vector<double> A;
+    std::vector<float> frag;
+    int rc = 0;
+    A.assign((size_t)MP * NK, 0.0);  // L (MP × NK)
+    for (int m = 0; m < 2 * N; ++m)
+        for (int j = 0; j < N; ++j) A[(size_t)m * NK + j] = Ld[(size_t)m * N + j];
+    fill_frag(frag, MP, NK, A);
+    rc |= upload(&c->d_Lfrag, frag);
+    A.assign((size_t)NK * MP, 0.0);  // Lᵀ (NK × MP)
+    for (int m = 0; m < 2 * N; ++m)
+        for (int j = 0; j < N; ++j) A[(size_t)j * MP + m] = Ld[(size_t)m * N + j];
+    fill_frag(frag, NK, MP, A);
+    rc |= upload(&c->d_LTfrag, frag);
+    A.assign((size_t)RP * NK, 0.0);  // F_topᵀ (RP × NK)
+    for (int n = 0; n < N; ++n)
+        for (int r = 0; r < RP; ++r) A[(size_t)r * NK + n] = F[(size_t)n * RP + r];
+    fill_frag(frag, RP, NK, A);
+    rc |= upload(&c->d_F1, frag);
+    A.assign((size_t)MP * RP, 0.0);  // F (MP × RP)
+    for (int m = 0; m < 2 * N; ++m)
+        for (int r = 0; r < RP; ++r) A[(size_t)m * RP + r] = F[(size_t)m * RP + r];
+    fill_frag(frag, MP, RP, A);
+    rc |= upload(&c->d_F2, frag);
+    std::vector<float> fb((size_t)N * RP), vr((size_t)N * RP);
+    for (int n = 0; n < N; ++n)
+        for (int r = 0; r < RP; ++r) {
+            fb[(size_t)n * RP + r] = (float)F[(size_t)(N + n) * RP + r];
+            vr[(size_t)n * RP + r] = (float)Vd[(size_t)n * RP + r];
+        }
+    rc |= upload(&c->d_Fbot, fb);
+    rc |= upload(&c->d_Vr, vr);
+    A.assign((size_t)NK * RP, 0.0);  // V_R (NK × RP), rows ≥ N zero
+    for (int n = 0; n < N; ++n)
+        for (int r = 0; r < RP; ++r) A[(size_t)n * RP + r] = Vd[(size_t)n * RP + r];
+    fill_frag(frag, NK, RP, A);
+    rc |= upload(&c->d_Vfrag, frag);
+    // initTrajectory basis: u = K⁻¹(1−c), w = K⁻¹c (fp32 LU, trajectory.py:77)
+    {
+        std::vector<float> rhs((size_t)N * 2), X((size_t)N * 2);
+        for (int n = 0; n < N; ++n) {
+            rhs[(size_t)n * 2] = 1.f - c->cvec[n];
+            rhs[(size_t)n * 2 + 1] = c->cvec[n];
+        }
+        if (!lu_solve_f32(N, c->K.data(), rhs.data(), 2, X.data())) {
+            irm_ctx_destroy(c);
+            return fail(IRM_EINVAL, "kernel matrix K is exactly singular in fp32 LU");
+        }
+        std::vector<float> u(N), w(N);
+        for (int n = 0; n < N; ++n) {
+            u[n] = X[(size_t)n * 2];
+            w[n] = X[(size_t)n * 2 + 1];
+        }
+        rc |= upload(&c->d_u, u);
+        rc |= upload(&c->d_w, w);
+    }
+    if (rc) {
+        std::string e = g_err;
+        irm_ctx_destroy(c);
+        return fail(IRM_ENOMEM, "%s", e.c_str());
+    }
+
+    // ---- kernel parameter template
+    KParams& kp = c->kp;
+    kp.N = N;
+    kp.D = D;
+    kp.R = R;
+    kp.NK = NK;
+    kp.MP = MP;
+    kp.RP = RP;
+    kp.O = 0;
+    kp.optimizer = p->optimizer;
+    kp.max_inner = p->max_inner_iteration;
+    kp.max_outer = p->max_outer_iteration;
+    kp.max_bls = p->max_bls_iteration;
+    kp.cvdl = p->constraint_violating_dependant_loss ? 1 : 0;
+    kp.llr = p->loop_loss_reduction;
+    kp.lci = p->lambda_constraint_increase;
+    kp.lsg0 = p->lambda_sg_constraint;
+    kp.ljl0 = p->lambda_jl_constraint;
+    kp.eps_p = p->eps_position;
+    kp.eps_v = p->eps_velocity;
+    kp.lmax = p->lambda_max_cost;
+    kp.lreg = p->lambda_reg;
+    kp.bls_lr0 = p->bls_lr_start;
+    kp.bls_a = p->bls_alpha;
+    kp.bls_bp = p->bls_beta_plus;
+    kp.bls_bm = p->bls_beta_minus;
+    kp.vmax = p->max_joint_velocity;
+    kp.pmax = p->max_joint_position;
+    kp.pmin = p->min_joint_position;
+    {  // trajectory.py:31-32, 221-222, 251 (Python doubles → fp32)
+        const double mean = 0.5 * ((double)p->max_joint_position + (double)p->min_joint_position);
+        const double stdp = 0.5 * ((double)p->max_joint_position - mean);
+        kp.mean_pos = (float)mean;
+        kp.std_pos = (float)stdp;
+        kp.std2 = kp.std_pos * kp.std_pos;
+        kp.vmax2 = kp.vmax * kp.vmax;
+        kp.thr_hi = (float)((double)p->joint_safety_limit * (double)p->max_joint_position);
+        kp.thr_lo = (float)((double)p->joint_safety_limit * (double)p->min_joint_position);
+        kp.thr_v = (float)((double)p->joint_safety_limit * (double)p->max_joint_velocity);
+        kp.invN = 1.f / (float)N;
+        kp.inv_std_pos = 1.f / kp.std_pos;
+        kp.inv_vmax = 1.f / kp.vmax;
+        kp.inv_std2 = 1.f / kp.std2;
+        kp.inv_vmax2 = 1.f / kp.vmax2;
+        kp.Nmagic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)N - 1) / (uint64_t)N);
+        kp.NDmagic = (uint32_t)((((uint64_t)1 << 32) + (uint64_t)(N * D) - 1) / (uint64_t)(N * D));
+    }
+    for (int i = 0; i < IRM_MAX_LR; ++i) kp.gd_lr[i] = p->gd_lr[i];
+    for (int i = 0; i < IRM_MAX_JOINTS; ++i) kp.link[i] = p->link_length[i];
+    {
+        std::vector<double> Jd((size_t)D * D), JtJ((size_t)D * D, 0.0);
+        for (int i = 0; i < D * D; ++i) Jd[i] = p->jac[i];
+        for (int a = 0; a < D; ++a)
+            for (int b = 0; b < D; ++b) {
+                double s = 0.0;
+                for (int k = 0; k < D; ++k) s += Jd[(size_t)k * D + a] * Jd[(size_t)k * D + b];
+                JtJ[(size_t)a * D + b] = s;
+            }
+        std::vector<float> eye((size_t)D * D, 0.f), Jinv((size_t)D * D);
+        for (int i = 0; i < D; ++i) eye[(size_t)i * D + i] = 1.f;
+        if (!lu_solve_f32(D, p->jac, eye.data(), D, Jinv.data())) {
+            irm_ctx_destroy(c);
+            return fail(IRM_EINVAL, "J is singular");
+        }
+        for (int i = 0; i < D * D; ++i) {
+            kp.J[i] = p->jac[i];
+            kp.JtJ[i] = (float)JtJ[i];
+            kp.Jinv[i] = Jinv[i];
+        }
+    }
+    kp.Lfrag = c->d_Lfrag;
+    kp.LTfrag = c->d_LTfrag;
+    kp.F1frag = c->d_F1;
+    kp.F2frag = c->d_F2;
+    kp.Fbot = c->d_Fbot;
+    kp.Vr = c->d_Vr;
+    kp.Vfrag = c->d_Vfrag;
+    kp.uvec = c->d_u;
+    kp.wvec = c->d_w;
+    kp.lam_max = p->lambda_max_cost;
+    kp.one_m_lmax = (float)(1.0 - (double)p->lambda_max_cost);
+    kp.record_series = p->record_series ? 1 : 0;
+    c->max_series = p->max_series > 0 ? p->max_series : 1 + p->max_outer_iteration * p->max_inner_iteration;
+    kp.max_series = c->max_series;
+
+    {
+        KParams probe = c->kp;
+        probe.O = IRM_MAX_OBSTACLES;
+        c->tb_opt = choose_shape(c, 1 << 20, true, probe, &c->lds_opt);
+        c->ops_lds = probe.ops_in_lds;
+    }
+    if (c->tb_opt <= 0) {
+        irm_ctx_destroy(c);
+        return fail(IRM_EINVAL, "configuration N=%d D=%d R=%d does not fit the 160 KiB LDS", N, D, R);
+    }
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        irm_ctx_destroy(c);
+        return fail(IRM_EDEVICE, "hipStreamCreate failed");
+    }
+    *out = c;
+    return IRM_OK;
+}
+
+void irm_ctx_destroy(irm_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->p.device);
+    float* bufs[] = {c->d_Lfrag, c->d_LTfrag, c->d_F1, c->d_F2, c->d_Fbot, c->d_Vr, c->d_Vfrag, c->d_u, c->d_w};
+    for (float* b : bufs)
+        if (b) (void)hipFree(b);
+    if (c->d_io) (void)hipFree(c->d_io);
+    if (c->d_prof) (void)hipFree(c->d_prof);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int irm_get_info(const irm_ctx* c, irm_info* out) {
+    if (!c || !out) return fail(IRM_EINVAL, "irm_get_info: null argument");
+    memset(out, 0, sizeof(*out));
+    out->abi_version = IRM_ABI_VERSION;
+    out->n_timesteps = c->N;
+    out->n_joints = c->D;
+    out->operator_rank = c->R;
+    out->operator_trunc = c->trunc;
+    out->traj_per_block = c->tb_opt;
+    out->num_cus = c->num_cus;
+    out->lds_bytes_optimize = c->lds_opt;
+    snprintf(out->device_name, sizeof(out->device_name), "%s", c->name);
+    snprintf(out->arch, sizeof(out->arch), "%s", c->arch);
+    return IRM_OK;
+}
+
+int32_t irm_series_capacity(const irm_ctx* c) { return c ? c->max_series : 0; }
+
+int irm_debug_phase_profile(irm_ctx* c, uint64_t* out, int32_t max_blocks) {
+    if (!c || !out) return fail(IRM_EINVAL, "null argument");
+#ifdef IRM_PHASE_PROFILE
+    if (set_device(c)) return IRM_EDEVICE;
+    const int n = std::min(max_blocks, c->prof_blocks);
+    if (n <= 0 || !c->d_prof) return 0;
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, c->d_prof, (size_t)n * irm::kProfPhases * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return n;
+#else
+    (void)max_blocks;
+    return fail(IRM_EINVAL, "library built without IRM_PHASE_PROFILE");
+#endif
+}
+
+int irm_kernel_matrices(const irm_ctx* c, float* t, float* km, float* dkm, float* jac) {
+    if (!c) return fail(IRM_EINVAL, "null context");
+    if (t) memcpy(t, c->t.data(), sizeof(float) * c->N);
+    if (km) memcpy(km, c->K.data(), sizeof(float) * c->K.size());
+    if (dkm) memcpy(dkm, c->dK.data(), sizeof(float) * c->dK.size());
+    if (jac) memcpy(jac, c->J.data(), sizeof(float) * c->J.size());
+    return IRM_OK;
+}
+
+// ----------------------------------------------------- host-pointer calls
+namespace {
+
+struct Stage {
+    irm_ctx* c;
+    size_t off = 0;
+    char* base() { return (char*)c->d_io; }
+    // reserve 256-B aligned slice
+    size_t take(size_t bytes) {
+        size_t o = off;
+        off += (bytes + 255) & ~(size_t)255;
+        return o;
+    }
+};
+
+int check_obs(int O) {
+    if (O < 0 || O > IRM_MAX_OBSTACLES) return fail(IRM_EINVAL, "n_obstacles=%d outside [0, %d]", O, IRM_MAX_OBSTACLES);
+    return 0;
+}
+
+// Run one forward-family kernel on B host trajectories.
+int run_forward(irm_ctx* c, int mode, const float* alpha, const float* start, const float* goal, const float* obs,
+                int O, int B, float lsg, float ljl, float lmax, int which, float* out0, float* out1, uint8_t* ok) {
+    if (set_device(c)) return IRM_EDEVICE;
+    if (B < 0 || !alpha) return fail(IRM_EINVAL, "bad batch arguments");
+    if (check_obs(O)) return IRM_EINVAL;
+    if (B == 0) return IRM_OK;
+    const int N = c->N, D = c->D;
+    const size_t nd = (size_t)B * N * D;
+    Stage st{c};
+    const size_t o_alpha = st.take(nd * 4), o_s = st.take((size_t)B * D * 4), o_g = st.take((size_t)B * D * 4),
+                 o_obs = st.take((size_t)std::max(O, 1) * 8), o_out0 = st.take(std::max(nd, (size_t)B * 11) * 4),
+                 o_out1 = st.take(nd * 4), o_ok = st.take((size_t)B);
+    if (ensure_io(c, st.off)) return IRM_ENOMEM;
+    char* d = st.base();
+    hipStream_t s = c->stream;
+    std::vector<float> zeros;
+    if (!start || !goal) zeros.assign((size_t)B * D, 0.f);
+    HIP_TRY(hipMemcpyAsync(d + o_alpha, alpha, nd * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d + o_s, start ? start : zeros.data(), (size_t)B * D * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d + o_g, goal ? goal : zeros.data(), (size_t)B * D * 4, hipMemcpyHostToDevice, s));
+    if (O > 0 && obs) HIP_TRY(hipMemcpyAsync(d + o_obs, obs, (size_t)O * 8, hipMemcpyHostToDevice, s));
+    KParams kp = c->kp;
+    kp.B = B;
+    kp.O = (obs ? O : 0);
+    kp.obs_stride = 0;
+    kp.alpha0 = (const float*)(d + o_alpha);
+    kp.start = (const float*)(d + o_s);
+    kp.goal = (const float*)(d + o_g);
+    kp.obstacles = (const float*)(d + o_obs);
+    kp.lam_sg = lsg;
+    kp.lam_jl = ljl;
+    kp.lam_max = lmax;
+    kp.one_m_lmax = (float)(1.0 - (double)lmax);
+    kp.which = which;
+    kp.out0 = (float*)(d + o_out0);
+    kp.out1 = (float*)(d + o_out1);
+    kp.out_ok = (uint8_t*)(d + o_ok);
+    if (choose_shape(c, B, false, kp, nullptr) <= 0) return fail(IRM_EINVAL, "no workgroup shape fits LDS");
+    HIP_TRY(irm::launch_forward(kp, mode, s));
+    if (out0) {
+        size_t bytes = (mode == 0) ? nd * 4 : (mode == 3 ? (size_t)B * 11 * 4 : (size_t)B * 4);
+        HIP_TRY(hipMemcpyAsync(out0, d + o_out0, bytes, hipMemcpyDeviceToHost, s));
+    }
+    if (out1) HIP_TRY(hipMemcpyAsync(out1, d + o_out1, nd * 4, hipMemcpyDeviceToHost, s));
+    if (ok) HIP_TRY(hipMemcpyAsync(ok, d + o_ok, (size_t)B, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return IRM_OK;
+}
+
+}  // namespace
+
+int irm_evaluate(irm_ctx* c, const float* alpha, int32_t B, int32_t which, float* out) {
+    if (!c || !out) return fail(IRM_EINVAL, "irm_evaluate: null argument");
+    return run_forward(c, 0, alpha, nullptr, nullptr, nullptr, 0, B, 0.f, 0.f, 0.f, which ? 1 : 0, out, nullptr,
+                       nullptr);
+}
+
+int irm_eval_cost(irm_ctx* c, const float* alpha, const float* start, const float* goal, const float* obstacles,
+                  int32_t O, int32_t B, float lsg, float ljl, float lmax, float* cost_out) {
+    if (!c || !cost_out || !start || !goal) return fail(IRM_EINVAL, "irm_eval_cost: null argument");
+    return run_forward(c, 1, alpha, start, goal, obstacles, O, B, lsg, ljl, lmax, 0, cost_out, nullptr, nullptr);
+}
+
+int irm_eval_cost_grad(irm_ctx* c, const float* alpha, const float* start, const float* goal, const float* obstacles,
+                       int32_t O, int32_t B, float lsg, float ljl, float lmax, float* grad_out, float* cost_out) {
+    if (!c || !grad_out || !start || !goal) return fail(IRM_EINVAL, "irm_eval_cost_grad: null argument");
+    return run_forward(c, 2, alpha, start, goal, obstacles, O, B, lsg, ljl, lmax, 0, cost_out, grad_out, nullptr);
+}
+
+int irm_constraints(irm_ctx* c, const float* alpha, const float* start, const float* goal, int32_t B, uint8_t* ok_out,
+                    float* report_out) {
+    if (!c || !ok_out || !start || !goal) return fail(IRM_EINVAL, "irm_constraints: null argument");
+    return run_forward(c, 3, alpha, start, goal, nullptr, 0, B, 0.f, 0.f, 0.f, 0, report_out, nullptr, ok_out);
+}
+
+int irm_fk(irm_ctx* c, const float* traj, int32_t B, float* pos_out, float* jac_out) {
+    if (!c || !traj || !pos_out) return fail(IRM_EINVAL, "irm_fk: null argument");
+    if (set_device(c)) return IRM_EDEVICE;
+    if (B <= 0) return B == 0 ? IRM_OK : fail(IRM_EINVAL, "negative batch");
+    const int N = c->N, D = c->D;
+    const size_t nd = (size_t)B * N * D;
+    Stage st{c};
+    const size_t o_q = st.take(nd * 4), o_p = st.take((size_t)B * 2 * N * 4), o_j = st.take(2 * nd * 4);
+    if (ensure_io(c, st.off)) return IRM_ENOMEM;
+    char* d = st.base();
+    KParams kp = c->kp;
+    kp.B = B;
+    HIP_TRY(hipMemcpyAsync(d + o_q, traj, nd * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(irm::launch_fk(kp, (const float*)(d + o_q), (float*)(d + o_p), jac_out ? (float*)(d + o_j) : nullptr,
+                           c->stream));
+    HIP_TRY(hipMemcpyAsync(pos_out, d + o_p, (size_t)B * 2 * N * 4, hipMemcpyDeviceToHost, c->stream));
+    if (jac_out) HIP_TRY(hipMemcpyAsync(jac_out, d + o_j, 2 * nd * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return IRM_OK;
+}
+
+int irm_compute_cost_vg(irm_ctx* c, const float* f, const float* obstacles, int32_t O, int32_t B, float* cost_v,
+                        float* cost_g) {
+    if (!c || !f || !cost_v || (O > 0 && !obstacles)) return fail(IRM_EINVAL, "irm_compute_cost_vg: null argument");
+    if (check_obs(O)) return IRM_EINVAL;
+    if (set_device(c)) return IRM_EDEVICE;
+    if (B <= 0) return B == 0 ? IRM_OK : fail(IRM_EINVAL, "negative batch");
+    const int N = c->N;
+    Stage st{c};
+    const size_t o_f = st.take((size_t)B * 2 * N * 4), o_o = st.take((size_t)std::max(O, 1) * 8),
+                 o_v = st.take((size_t)B * N * 4), o_g = st.take((size_t)B * 2 * N * 4);
+    if (ensure_io(c, st.off)) return IRM_ENOMEM;
+    char* d = st.base();
+    KParams kp = c->kp;
+    kp.B = B;
+    kp.O = O;
+    kp.obstacles = (const float*)(d + o_o);
+    HIP_TRY(hipMemcpyAsync(d + o_f, f, (size_t)B * 2 * N * 4, hipMemcpyHostToDevice, c->stream));
+    if (O > 0) HIP_TRY(hipMemcpyAsync(d + o_o, obstacles, (size_t)O * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(irm::launch_cost_vg(kp, (const float*)(d + o_f), (float*)(d + o_v), cost_g ? (float*)(d + o_g) : nullptr,
+                                c->stream));
+    HIP_TRY(hipMemcpyAsync(cost_v, d + o_v, (size_t)B * N * 4, hipMemcpyDeviceToHost, c->stream));
+    if (cost_g) HIP_TRY(hipMemcpyAsync(cost_g, d + o_g, (size_t)B * 2 * N * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return IRM_OK;
+}
+
+int irm_init_alpha(irm_ctx* c, const float* start, const float* goal, int32_t B, float* alpha_out) {
+    if (!c || !start || !goal || !alpha_out) return fail(IRM_EINVAL, "irm_init_alpha: null argument");
+    if (set_device(c)) return IRM_EDEVICE;
+    if (B <= 0) return B == 0 ? IRM_OK : fail(IRM_EINVAL, "negative batch");
+    const int N = c->N, D = c->D;
+    const size_t nd = (size_t)B * N * D;
+    Stage st{c};
+    const size_t o_s = st.take((size_t)B * D * 4), o_g = st.take((size_t)B * D * 4), o_a = st.take(nd * 4);
+    if (ensure_io(c, st.off)) return IRM_ENOMEM;
+    char* d = st.base();
+    KParams kp = c->kp;
+    kp.B = B;
+    kp.start = (const float*)(d + o_s);
+    kp.goal = (const float*)(d + o_g);
+    HIP_TRY(hipMemcpyAsync(d + o_s, start, (size_t)B * D * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d + o_g, goal, (size_t)B * D * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(irm::launch_init_alpha(kp, (float*)(d + o_a), c->stream));
+    HIP_TRY(hipMemcpyAsync(alpha_out, d + o_a, nd * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return IRM_OK;
+}
+
+int irm_optimize_batch_dev(irm_ctx* c, const irm_batch_dev* a, void* stream) {
+    if (!c || !a) return fail(IRM_EINVAL, "irm_optimize_batch_dev: null argument");
+    if (a->batch < 0 || !a->start || !a->goal) return fail(IRM_EINVAL, "bad batch arguments");
+    if (check_obs(a->n_obstacles)) return IRM_EINVAL;
+    if (a->n_obstacles > 0 && !a->obstacles) return fail(IRM_EINVAL, "obstacles pointer missing");
+    if (set_device(c)) return IRM_EDEVICE;
+    if (a->batch == 0) return IRM_OK;
+    KParams kp = c->kp;
+    kp.B = a->batch;
+    kp.O = a->n_obstacles;
+    kp.obs_stride = a->obstacle_stride;
+    kp.alpha0 = a->alpha0;
+    kp.start = a->start;
+    kp.goal = a->goal;
+    kp.obstacles = a->obstacles;
+    kp.alpha_out = a->alpha_out;
+    kp.traj_out = a->traj_out;
+    kp.stats = a->stats_out;
+    kp.series = a->series_out;
+    if (choose_shape(c, a->batch, true, kp, nullptr) <= 0) return fail(IRM_EINVAL, "no workgroup shape fits LDS");
+#ifdef IRM_PHASE_PROFILE
+    {
+        const int grid = (a->batch + kp.TB - 1) / kp.TB;
+        if (grid > c->prof_cap) {
+            if (c->d_prof) (void)hipFree(c->d_prof);
+            c->d_prof = nullptr;
+            HIP_TRY(hipMalloc(&c->d_prof, (size_t)grid * irm::kProfPhases * sizeof(unsigned long long)));
+            c->prof_cap = grid;
+        }
+        c->prof_blocks = grid;
+        kp.prof = c->d_prof;
+    }
+#endif
+    HIP_TRY(irm::launch_optimize(kp, (hipStream_t)stream));
+    return IRM_OK;
+}
+
+int irm_optimize_batch(irm_ctx* c, const float* alpha0, const float* start, const float* goal, const float* obstacles,
+                       int32_t O, int32_t obstacle_stride, int32_t B, float* alpha_out, float* traj_out,
+                       irm_stats* stats_out, float* series_out) {
+    if (!c || !start || !goal) return fail(IRM_EINVAL, "irm_optimize_batch: null argument");
+    if (check_obs(O)) return IRM_EINVAL;
+    if (set_device(c)) return IRM_EDEVICE;
+    if (B <= 0) return B == 0 ? IRM_OK : fail(IRM_EINVAL, "negative batch");
+    const int N = c->N, D = c->D;
+    const size_t nd = (size_t)B * N * D;
+    const size_t nobs = obstacle_stride ? (size_t)B * obstacle_stride : (size_t)O * 2;
+    const size_t nser = series_out ? (size_t)B * c->max_series * N * D : 0;
+    Stage st{c};
+    const size_t o_a0 = st.take(nd * 4), o_s = st.take((size_t)B * D * 4), o_g = st.take((size_t)B * D * 4),
+                 o_o = st.take(std::max<size_t>(nobs, 1) * 4), o_ao = st.take(nd * 4), o_to = st.take(nd * 4),
+                 o_st = st.take((size_t)B * sizeof(irm_stats)), o_se = st.take(std::max<size_t>(nser, 1) * 4);
+    if (ensure_io(c, st.off)) return IRM_ENOMEM;
+    char* d = st.base();
+    hipStream_t s = c->stream;
+    if (alpha0) HIP_TRY(hipMemcpyAsync(d + o_a0, alpha0, nd * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d + o_s, start, (size_t)B * D * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d + o_g, goal, (size_t)B * D * 4, hipMemcpyHostToDevice, s));
+    if (nobs && obstacles) HIP_TRY(hipMemcpyAsync(d + o_o, obstacles, nobs * 4, hipMemcpyHostToDevice, s));
+    irm_batch_dev a{};
+    a.alpha0 = alpha0 ? (const float*)(d + o_a0) : nullptr;
+    a.start = (const float*)(d + o_s);
+    a.goal = (const float*)(d + o_g);
+    a.obstacles = (const float*)(d + o_o);
+    a.n_obstacles = O;
+    a.obstacle_stride = obstacle_stride;
+    a.batch = B;
+    a.alpha_out = (float*)(d + o_ao);
+    a.traj_out = (float*)(d + o_to);
+    a.stats_out = (irm_stats*)(d + o_st);
+    a.series_out = series_out ? (float*)(d + o_se) : nullptr;
+    KParams save = c->kp;
+    if (series_out) c->kp.record_series = 1;
+    int rc = irm_optimize_batch_dev(c, &a, s);
+    c->kp = save;
+    if (rc) return rc;
+    if (alpha_out) HIP_TRY(hipMemcpyAsync(alpha_out, d + o_ao, nd * 4, hipMemcpyDeviceToHost, s));
+    if (traj_out) HIP_TRY(hipMemcpyAsync(traj_out, d + o_to, nd * 4, hipMemcpyDeviceToHost, s));
+    if (stats_out) HIP_TRY(hipMemcpyAsync(stats_out, d + o_st, (size_t)B * sizeof(irm_stats), hipMemcpyDeviceToHost, s));
+    if (series_out) HIP_TRY(hipMemcpyAsync(series_out, d + o_se, nser * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return IRM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,1129 @@
+// irm_kernels.hip — gfx950 (CDNA4) kernels for the RKHS trajectory optimiser.
+//
+// Hot path of simongroeger/irm_motion_planning: optimizer_GD.py:386-445 and
+// optimizer_BLS.py:126-213 over trajectory.py:271-297 / robot.py:29-87 /
+// environment.py:32-58.  DESIGN.md describes the formulation:
+//   * the optimiser state is kept in trajectory space, T = K·α·J and
+//     V = dK·α·J (the reference keeps α, |α|≈1e3, which cancels in fp32);
+//   * the α-space step α' = c·α − s·G, G = (Kᵀa + dKᵀb)Jᵀ, becomes
+//     [T';V'] = c·[T;V] − s·L·Lᵀ[a;b]·JᵀJ with L = [K;dK];
+//   * L·Lᵀ is applied as F·(Fᵀ[a;b]) with F = L·V_R (V_R = top-R right
+//     singular vectors of L; R = N, V = I is the exact dense operator);
+//   * both contractions run on v_mfma_f32_16x16x4_f32 with the TB·D
+//     (trajectory, joint) columns of a workgroup as the 16 MFMA columns;
+//   * one lane per (trajectory, waypoint): the trajectory's waypoints and
+//     velocities live in that lane's registers for the whole optimisation;
+//     FK / obstacle potential / penalties are VALU, per-trajectory
+//     reductions are DPP wave reductions + a cross-wave LDS combine;
+//   * the GD / BLS control flow is a per-trajectory state machine whose
+//     scalar state is replicated in the trajectory's lanes (every lane takes
+//     the same decision from the same reduced values), inside one persistent
+//     launch per optimize().
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "irm_kernels.hpp"
+
+namespace irm {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------ LDS planning
+__host__ __device__ static inline int al4(int x) { return (x + 3) & ~3; }
+
+__host__ __device__ Plan plan_lds(const KParams& p, bool ops_lds, bool optimizer) {
+    Plan L{};
+    int off = 0;
+    auto take = [&](int n) {
+        int o = off;
+        off += al4(n);
+        return o;
+    };
+    const int N = p.N, TB = p.TB, nw = p.BT / 64;
+    L.f1 = L.f2 = L.fb = 0;
+    if (optimizer && ops_lds) {
+        L.f1 = take((int)frag_floats(p.RP, p.NK));
+        L.f2 = take((int)frag_floats(p.MP, p.RP));
+        L.fb = take(N * p.RP);
+    }
+    if (optimizer) {
+        L.X = take(p.NK * kCols);
+        L.Bs = take(N * kCols);
+    } else {
+        L.X = take(p.MP * kCols);  // [a; b] stacked (rows 0..N-1, N..2N-1)
+        L.Bs = L.X + N * kCols;
+    }
+    L.dP = take(p.MP * kCols);
+    if (optimizer) {
+        L.Ypart = take(p.nsplit * p.RP * kCols);
+        L.Ydir = take(p.RP * kCols);
+        L.Ymix = take(p.RP * kCols);
+        L.Yacc = take(p.RP * kCols);
+    } else {
+        L.Ypart = L.Ydir = L.Ymix = L.Yacc = 0;
+    }
+    L.red = take(nw * 10);
+    L.sg = take(TB * 4);
+    L.wp = take(nw * p.D * p.D);
+    L.flags = take(2 * TB);
+    L.act = take(N + 4);
+    L.list = take(N + 4);
+    L.obs = take((p.obs_stride ? TB : 1) * p.O * 2 + 4);
+    L.total = off;
+    return L;
+}
+
+// ------------------------------------------------------------ wave helpers
+// DPP row reductions (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+// row_mirror) leave each 16-lane row reduced in all its lanes; the four
+// rows are then combined from v_readlane (uniform result, no LDS).
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v) {
+    return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ float lanef(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float wred_sum(float v) {
+    v += dppf<0xB1>(v);
+    v += dppf<0x4E>(v);
+    v += dppf<0x141>(v);
+    v += dppf<0x140>(v);
+    return (lanef(v, 0) + lanef(v, 16)) + (lanef(v, 32) + lanef(v, 48));
+}
+__device__ __forceinline__ float wred_max(float v) {
+    v = fmaxf(v, dppf<0xB1>(v));
+    v = fmaxf(v, dppf<0x4E>(v));
+    v = fmaxf(v, dppf<0x141>(v));
+    v = fmaxf(v, dppf<0x140>(v));
+    return fmaxf(fmaxf(lanef(v, 0), lanef(v, 16)), fmaxf(lanef(v, 32), lanef(v, 48)));
+}
+__device__ __forceinline__ float wred_min(float v) {
+    v = fminf(v, dppf<0xB1>(v));
+    v = fminf(v, dppf<0x4E>(v));
+    v = fminf(v, dppf<0x141>(v));
+    v = fminf(v, dppf<0x140>(v));
+    return fminf(fminf(lanef(v, 0), lanef(v, 16)), fminf(lanef(v, 32), lanef(v, 48)));
+}
+// max with first-index tie break (jnp.argmax, trajectory.py:97)
+__device__ __forceinline__ void amax_step(float& v, int& i, float ov, int oi) {
+    if (ov > v || (ov == v && oi < i)) {
+        v = ov;
+        i = oi;
+    }
+}
+template <int CTRL>
+__device__ __forceinline__ void amax_dpp(float& v, int& i) {
+    float ov = dppf<CTRL>(v);
+    int oi = dppi<CTRL>(i);
+    amax_step(v, i, ov, oi);
+}
+__device__ __forceinline__ void wred_argmax(float& v, int& i) {
+    amax_dpp<0xB1>(v, i);
+    amax_dpp<0x4E>(v, i);
+    amax_dpp<0x141>(v, i);
+    amax_dpp<0x140>(v, i);
+    float bv = lanef(v, 0);
+    int bi = __builtin_amdgcn_readlane(i, 0);
+#pragma unroll
+    for (int r = 16; r < 64; r += 16) amax_step(bv, bi, lanef(v, r), __builtin_amdgcn_readlane(i, r));
+    v = bv;
+    i = bi;
+}
+
+// ---------------------------------------------------- phase profiler (diag)
+// Built with -DIRM_PHASE_PROFILE: thread 0 of each workgroup accumulates the
+// shader-clock cycles (s_memtime) between consecutive stamps per phase into
+// P.prof[block][phase].  In the shipped build every stamp is empty.
+struct Prof {
+#ifdef IRM_PHASE_PROFILE
+    unsigned long long last, acc[kProfPhases];
+    __device__ __forceinline__ void init() {
+        last = __builtin_amdgcn_s_memtime();
+#pragma unroll
+        for (int i = 0; i < kProfPhases; ++i) acc[i] = 0;
+    }
+    __device__ __forceinline__ void stamp(int ph) {
+        unsigned long long now = __builtin_amdgcn_s_memtime();
+        acc[ph] += now - last;
+        last = now;
+    }
+    __device__ __forceinline__ void flush(unsigned long long* out) {
+        if (out)
+            for (int i = 0; i < kProfPhases; ++i) out[(size_t)blockIdx.x * kProfPhases + i] = acc[i];
+    }
+#else
+    __device__ __forceinline__ void init() {}
+    __device__ __forceinline__ void stamp(int) {}
+    __device__ __forceinline__ void flush(unsigned long long*) {}
+#endif
+};
+#define IRM_STAMP(ph)                         \
+    do {                                      \
+        if (threadIdx.x == 0) prof.stamp(ph); \
+    } while (0)
+
+// ---------------------------------------------------------- MFMA contraction
+// acc(16×16 tile) = Σ_{kq∈[kq0,kq1)} A[tile, kq] · X[16kq .. 16kq+15][0..15]
+// A: 16x16x4 A-fragments (frag_index layout), one float4 per lane = 4 k-steps.
+// X: LDS, row stride 16 floats (one row per k); lane l reads row 4j+(l>>4),
+// column l&15 of each k-step: 64 consecutive floats, conflict-free.
+__device__ __forceinline__ f32x4 mma_tile(const float* __restrict__ A, int KQ, int tile, int kq0, int kq1,
+                                          const float* __restrict__ X) {
+    const int lane = threadIdx.x & 63;
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    const float* xl = X + (lane >> 4) * 16 + (lane & 15);
+    const f32x4* ap = reinterpret_cast<const f32x4*>(A) + ((size_t)tile * KQ) * 64 + lane;
+    for (int kq = kq0; kq < kq1; ++kq) {
+        f32x4 a = ap[(size_t)kq * 64];
+        const float* xb = xl + kq * 256;
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], xb[0], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], xb[64], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], xb[128], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], xb[192], acc1, 0, 0, 0);
+    }
+    return acc0 + acc1;
+}
+
+// D layout of 16x16x4: lane l holds rows 4*(l>>4)+i, column l&15.
+__device__ __forceinline__ void store_tile(float* out, int tile, f32x4 acc, unsigned colmask, int rows) {
+    const int lane = threadIdx.x & 63;
+    const int col = lane & 15;
+    if (!((colmask >> col) & 1u)) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        int row = tile * 16 + 4 * (lane >> 4) + i;
+        if (row < rows) out[row * 16 + col] = acc[i];
+    }
+}
+
+// out[MT tiles] = A · X over all K; tiles dealt round-robin to the waves.
+__device__ void mma_rows(const float* A, int MT, int KQ, const float* X, float* out, unsigned colmask, int rows,
+                         int wave, int nwaves) {
+    for (int tile = wave; tile < MT; tile += nwaves) {
+        f32x4 acc = mma_tile(A, KQ, tile, 0, KQ, X);
+        store_tile(out, tile, acc, colmask, rows);
+    }
+}
+
+// ------------------------------------------------ per-waypoint physics
+template <int D>
+struct WP {
+    float cv, gx, gy;        // obstacle potential and its gradient at the end effector
+    float jp, jv;            // masked joint-position / joint-velocity penalty terms
+    float tx, tn, va;        // max/min joint position, max |joint velocity|
+    float jx[D], jy[D];      // end-effector Jacobian row
+};
+
+// robot.py:29-36 (fk), 75-87 (jacobian); environment.py:46-58
+// (compute_cost_vg); trajectory.py:215-227, 245-255 (penalty elements).
+template <int D>
+__device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)[D], const float (&v)[D],
+                                              const float* __restrict__ ob, WP<D>& w) {
+    float cum = 0.f, fx = 0.f, fy = 0.f, Sx = 0.f, Sy = 0.f;
+    float xs[D], ys[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        cum += q[d];
+        float sn, cs;
+        sincosf(cum, &sn, &cs);
+        fx += P.link[d] * cs;
+        fy += P.link[d] * sn;
+        xs[d] = -(P.link[d] * sn);
+        ys[d] = P.link[d] * cs;
+        Sx += xs[d];
+        Sy += ys[d];
+    }
+    float Cx = 0.f, Cy = 0.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        Cx += xs[d];
+        Cy += ys[d];
+        w.jx[d] = (xs[d] + Sx) - Cx;
+        w.jy[d] = (ys[d] + Sy) - Cy;
+    }
+    float cv = 0.f, ax = 0.f, ay = 0.f;
+    for (int o = 0; o < P.O; ++o) {
+        const float dx = fx - ob[2 * o], dy = fy - ob[2 * o + 1];
+        const float r2 = dx * dx + dy * dy;
+        const float den = 0.5f + 0.5f * r2;
+        const float inv = __builtin_amdgcn_rcpf(den);
+        cv += 0.8f * inv;
+        const float i2 = inv * inv;
+        ax += (-0.8f * dx) * i2;
+        ay += (-0.8f * dy) * i2;
+    }
+    w.cv = cv;
+    w.gx = ax;
+    w.gy = ay;
+    float jp = 0.f, jv = 0.f, tx = -INFINITY, tn = INFINITY, va = 0.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const float z = (q[d] - P.mean_pos) * P.inv_std_pos;
+        const bool m = (q[d] > P.thr_hi) || (q[d] < P.thr_lo);
+        jp += (P.cvdl && !m) ? 0.f : 0.5f * (z * z);
+        const float zv = v[d] * P.inv_vmax;
+        const bool mv = fabsf(v[d]) > P.thr_v;
+        jv += (P.cvdl && !mv) ? 0.f : 0.5f * (zv * zv);
+        tx = fmaxf(tx, q[d]);
+        tn = fminf(tn, q[d]);
+        va = fmaxf(va, fabsf(v[d]));
+    }
+    w.jp = jp;
+    w.jv = jv;
+    w.tx = tx;
+    w.tn = tn;
+    w.va = va;
+}
+
+// Gradient inputs a (→ Kᵀ) and b (→ dKᵀ) of one waypoint, trajectory.py:91-126
+// (obstacle), 191-212 (start/goal), 231-242 / 259-268 (joint limits).
+template <int D>
+__device__ __forceinline__ void grad_waypoint(const KParams& P, const WP<D>& w, const float (&q)[D],
+                                              const float (&v)[D], int n, int idx, float lsg, float ljl,
+                                              const float (&s)[D], const float (&g)[D], float (&a)[D],
+                                              float (&b)[D]) {
+    const int N = P.N;
+    const float wt = (n == idx ? P.lam_max : 0.f) + P.one_m_lmax * P.invN;
+    const float wx = wt * w.gx, wy = wt * w.gy;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        float sgp = 0.f, sgv = 0.f;
+        if (n == 0) {
+            sgp = q[d] - s[d];
+            sgv = v[d];
+        }
+        if (n == N - 1) {
+            sgp = q[d] - g[d];
+            sgv = v[d];
+        }
+        float jpg = 0.f, jvg = 0.f;
+        const bool m = (q[d] > P.thr_hi) || (q[d] < P.thr_lo);
+        if (!P.cvdl || m) jpg = ((q[d] - P.mean_pos) * P.inv_std2) * P.invN;
+        const bool mv = fabsf(v[d]) > P.thr_v;
+        if (!P.cvdl || mv) jvg = (v[d] * P.inv_vmax2) * P.invN;
+        a[d] = (wx * w.jx[d] + wy * w.jy[d]) + lsg * sgp + ljl * jpg;
+        b[d] = lsg * sgv + ljl * jvg;
+    }
+}
+
+// Result of one cost evaluation of one trajectory (reduced over waypoints).
+struct EvalOut {
+    float loss, ds, dg, vs, vg, tmax, tmin, vabs;
+    int idx;
+};
+
+// Wave-reduce this lane's waypoint terms; lane 0 of each wave stores the
+// partials, the lanes of rows 0 / N−1 store the start/goal terms.  Must be
+// reached by the whole wave (a wave never straddles two trajectories).
+template <int D>
+__device__ __forceinline__ void eval_partials(const KParams& P, bool live, const WP<D>& w, int n, int wave,
+                                              const float (&q)[D], const float (&v)[D], const float (&s)[D],
+                                              const float (&g)[D], float* red, float* sg, int t) {
+    float cmax = live ? w.cv : -INFINITY;
+    int cidx = live ? n : 0x7fffffff;
+    wred_argmax(cmax, cidx);
+    const float csum = wred_sum(live ? w.cv : 0.f);
+    const float jps = wred_sum(live ? w.jp : 0.f);
+    const float jvs = wred_sum(live ? w.jv : 0.f);
+    const float tx = wred_max(live ? w.tx : -INFINITY);
+    const float tn = wred_min(live ? w.tn : INFINITY);
+    const float va = wred_max(live ? w.va : 0.f);
+    if ((threadIdx.x & 63) == 0) {
+        float* r = red + wave * 10;
+        r[0] = cmax;
+        r[1] = __int_as_float(cidx);
+        r[2] = csum;
+        r[3] = jps;
+        r[4] = jvs;
+        r[5] = tx;
+        r[6] = tn;
+        r[7] = va;
+    }
+    if (live && (n == 0 || n == P.N - 1)) {  // trajectory.py:183-204 rows 0 and N−1
+        float a = 0.f, bb = 0.f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const float e = q[d] - (n == 0 ? s[d] : g[d]);
+            a += e * e;
+            bb += v[d] * v[d];
+        }
+        sg[t * 4 + (n == 0 ? 0 : 2)] = a;
+        sg[t * 4 + (n == 0 ? 1 : 3)] = bb;
+    }
+}
+
+// Combine the trajectory's wave partials (fixed order) into loss + stats.
+__device__ __forceinline__ EvalOut eval_finalize(const KParams& P, const float* red, const float* sg, int t,
+                                                 int wave0, int nwt, float lsg, float ljl) {
+    const float* r = red + wave0 * 10;
+    float cmax = r[0];
+    int cidx = __float_as_int(r[1]);
+    float csum = r[2], jps = r[3], jvs = r[4], tx = r[5], tn = r[6], va = r[7];
+    for (int w = 1; w < nwt; ++w) {
+        const float* q = red + (wave0 + w) * 10;
+        amax_step(cmax, cidx, q[0], __float_as_int(q[1]));
+        csum += q[2];
+        jps += q[3];
+        jvs += q[4];
+        tx = fmaxf(tx, q[5]);
+        tn = fminf(tn, q[6]);
+        va = fmaxf(va, q[7]);
+    }
+    const float a0 = sg[t * 4 + 0], b0 = sg[t * 4 + 1], a1 = sg[t * 4 + 2], b1 = sg[t * 4 + 3];
+    const float nN = (float)P.N;
+    const float sgpc = 0.5f * a0 + 0.5f * a1;                          // trajectory.py:187
+    const float sgvc = 0.5f * b0 + 0.5f * b1;                          // trajectory.py:203
+    const float toc = P.lam_max * cmax + P.one_m_lmax * (csum / nN);    // trajectory.py:85-87
+    EvalOut e;
+    e.loss = toc + lsg * (sgpc + sgvc) + ljl * (jps / nN + jvs / nN);  // trajectory.py:281
+    e.idx = cidx;
+    e.ds = sqrtf(a0);
+    e.dg = sqrtf(a1);
+    e.vs = sqrtf(b0);
+    e.vg = sqrtf(b1);
+    e.tmax = tx;
+    e.tmin = tn;
+    e.vabs = va;
+    return e;
+}
+
+// α0 of the block's trajectories into X[n][tD+d] (rows ≥ N / unused columns 0).
+template <int D>
+__device__ void stage_alpha(const KParams& P, int tb0, int ntb, float* X, int xrows) {
+    const int N = P.N;
+    for (int e = threadIdx.x; e < xrows * 16; e += P.BT) {
+        const int n = e >> 4, c = e & 15, t = c / D, d = c - t * D;
+        float val = 0.f;
+        if (n < N && t < ntb) {
+            const size_t b = (size_t)(tb0 + t);
+            if (P.alpha0) {
+                val = P.alpha0[(b * N + n) * D + d];
+            } else {  // trajectory.py:73-78 via K⁻¹(1−c), K⁻¹c (linearity of solve)
+                float sj = 0.f, gj = 0.f;
+                for (int e2 = 0; e2 < D; ++e2) {
+                    sj += P.start[b * D + e2] * P.Jinv[e2 * D + d];
+                    gj += P.goal[b * D + e2] * P.Jinv[e2 * D + d];
+                }
+                val = P.uvec[n] * sj + P.wvec[n] * gj;
+            }
+        }
+        X[e] = val;
+    }
+}
+
+template <int D>
+__device__ __forceinline__ float alpha0_at(const KParams& P, size_t b, int n, int k) {
+    if (P.alpha0) return P.alpha0[(b * P.N + n) * D + k];
+    float sj = 0.f, gj = 0.f;
+    for (int e2 = 0; e2 < D; ++e2) {
+        sj += P.start[b * D + e2] * P.Jinv[e2 * D + k];
+        gj += P.goal[b * D + e2] * P.Jinv[e2 * D + k];
+    }
+    return P.uvec[n] * sj + P.wvec[n] * gj;
+}
+
+// ------------------------------------------------------------ optimiser
+template <int D, int MAXT, bool OPS_LDS>
+__global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const Plan L = plan_lds(P, OPS_LDS, true);
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nwaves = P.BT >> 6;
+    const int N = P.N, NW = P.NW, TB = P.TB, RP = P.RP, MP = P.MP, NK = P.NK;
+    const int WPT = NW >> 6;            // waves per trajectory
+    const int t = wave / WPT;           // this lane's trajectory (wave-uniform)
+    const int n = tid - t * NW;         // this lane's waypoint
+    const int tb0 = blockIdx.x * TB;
+    const int ntb = min(TB, P.B - tb0);
+    if (ntb <= 0) return;
+    const bool tvalid = t < ntb;
+    const bool valid = tvalid && n < N;
+    const size_t b = (size_t)(tb0 + (tvalid ? t : 0));
+    const bool bls = (P.optimizer == IRM_OPT_BLS);
+    const bool rec = P.record_series && P.series;
+    Prof prof;
+    if (tid == 0) prof.init();
+
+    float* X = smem + L.X;
+    float* Bs = smem + L.Bs;
+    float* dP = smem + L.dP;
+    float* Ypart = smem + L.Ypart;
+    float* Ydir = smem + L.Ydir;
+    float* Ymix = smem + L.Ymix;
+    float* Yacc = smem + L.Yacc;
+    float* red = smem + L.red;
+    float* sg = smem + L.sg;
+    float* wp = smem + L.wp;
+    int* flags = reinterpret_cast<int*>(smem + L.flags);
+    int* act = reinterpret_cast<int*>(smem + L.act);
+    int* list = reinterpret_cast<int*>(smem + L.list);
+    float* obsL = smem + L.obs;
+    const float* F1 = P.F1frag;
+    const float* F2 = P.F2frag;
+    const float* Fb = P.Fbot;
+
+    const int KQ1 = NK / 16, MT1 = RP / 16;   // stage 1: (RP × NK)·(NK × 16)
+    const int KQ2 = RP / 16, MT2 = MP / 16;   // stage 2: (MP × RP)·(RP × 16)
+
+    // ----------------------------------------------------------- prologue
+    if (OPS_LDS) {
+        const int n1 = (int)frag_floats(RP, NK) / 4, n2 = (int)frag_floats(MP, RP) / 4, n3 = N * RP / 4;
+        const f32x4* g1 = reinterpret_cast<const f32x4*>(P.F1frag);
+        const f32x4* g2 = reinterpret_cast<const f32x4*>(P.F2frag);
+        const f32x4* g3 = reinterpret_cast<const f32x4*>(P.Fbot);
+        f32x4* l1 = reinterpret_cast<f32x4*>(smem + L.f1);
+        f32x4* l2 = reinterpret_cast<f32x4*>(smem + L.f2);
+        f32x4* l3 = reinterpret_cast<f32x4*>(smem + L.fb);
+        for (int e = tid; e < n1; e += P.BT) l1[e] = g1[e];
+        for (int e = tid; e < n2; e += P.BT) l2[e] = g2[e];
+        for (int e = tid; e < n3; e += P.BT) l3[e] = g3[e];
+        F1 = smem + L.f1;
+        F2 = smem + L.f2;
+        Fb = smem + L.fb;
+    }
+    {
+        const int nobs = (P.obs_stride ? TB : 1) * P.O * 2;
+        for (int e = tid; e < nobs; e += P.BT) {
+            float val = 0.f;
+            if (P.obs_stride) {
+                const int tt = e / (P.O * 2), r = e - tt * P.O * 2;
+                if (tt < ntb) val = P.obstacles[(size_t)(tb0 + tt) * P.obs_stride + r];
+            } else {
+                val = P.obstacles[e];
+            }
+            obsL[e] = val;
+        }
+    }
+    for (int e = tid; e < N * 16; e += P.BT) Bs[e] = 0.f;
+    for (int e = tid; e < RP * 16; e += P.BT) {
+        Ydir[e] = 0.f;
+        Ymix[e] = 0.f;
+        Yacc[e] = 0.f;
+    }
+    for (int e = tid; e < N; e += P.BT) act[e] = 0;
+    if (tid < TB) {
+        flags[tid] = 0;                          // needs a direction next round
+        flags[TB + tid] = (tid < ntb) ? 0 : 1;   // done
+    }
+    stage_alpha<D>(P, tb0, ntb, X, NK);
+    __syncthreads();
+    // T0 = (K·α0)·J, V0 = (dK·α0)·J  (trajectory.py:63-65)
+    mma_rows(P.Lfrag, MT2, KQ1, X, dP, 0xFFFFu, MP, wave, nwaves);
+    __syncthreads();
+    float q[D], v[D], s[D], g[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        q[k] = v[k] = 0.f;
+        s[k] = tvalid ? P.start[b * D + k] : 0.f;
+        g[k] = tvalid ? P.goal[b * D + k] : 0.f;
+    }
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            float a = 0.f, c = 0.f;
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                a += dP[n * 16 + t * D + d] * P.J[d * D + k];
+                c += dP[(N + n) * 16 + t * D + d] * P.J[d * D + k];
+            }
+            q[k] = a;
+            v[k] = c;
+        }
+        if (rec) {
+#pragma unroll
+            for (int k = 0; k < D; ++k) P.series[(b * P.max_series) * N * D + n * D + k] = q[k];
+        }
+    }
+    for (int e = tid; e < NK * 16; e += P.BT) X[e] = 0.f;
+    const float* obs = obsL + (P.obs_stride ? t * P.O * 2 : 0);
+
+    // replicated per-trajectory scalar state
+    float loss = 0.f, lsg = P.lsg0, ljl = P.ljl0, lr = 0.f, cprod = 1.f, gnorm = 1.f, anorm = 0.f;
+    float cfac = 1.f, step = 0.f;
+    float s_ds = 0.f, s_dg = 0.f, s_vs = 0.f, s_vg = 0.f, s_tmax = 0.f, s_tmin = 0.f, s_vabs = 0.f;
+    int phase = tvalid ? PH_OUTER_START : PH_DONE, outer = 0, inner = 0, trial = 0, needs_dir = 0;
+    irm_stats st{};
+    st.series_len = rec ? 1 : 0;
+    __syncthreads();
+    IRM_STAMP(14);
+
+    const unsigned tmask = (1u << D) - 1u;
+    for (;;) {
+        // ------------------------------------------------ direction (stage 1+2)
+        unsigned dirmask = 0;
+        for (int tt = 0; tt < ntb; ++tt)
+            if (flags[tt]) dirmask |= tmask << (tt * D);
+        IRM_STAMP(4);
+        if (dirmask) {
+            // active sparse rows of b (start/goal velocity rows, masked velocity-limit rows)
+            if (wave == nwaves - 1) {
+                const int lane = tid & 63;
+                int cnt = 0;
+                for (int base = 0; base < N; base += 64) {
+                    const int nn = base + lane;
+                    const bool f = (nn < N) && act[nn];
+                    const unsigned long long m = __ballot(f);
+                    if (f) list[cnt + __popcll(m & ((1ull << lane) - 1ull))] = nn;
+                    cnt += __popcll(m);
+                }
+                if (lane == 0) list[N] = cnt;
+            }
+            // stage 1: Ypart[s] = F_topᵀ(RP × NK) · a   (split-K over the waves)
+            for (int u = wave; u < MT1 * P.nsplit; u += nwaves) {
+                const int tile = u % MT1, sp = u / MT1;
+                const int kq0 = (KQ1 * sp) / P.nsplit, kq1 = (KQ1 * (sp + 1)) / P.nsplit;
+                f32x4 acc = mma_tile(F1, KQ1, tile, kq0, kq1, X);
+                store_tile(Ypart + sp * RP * 16, tile, acc, 0xFFFFu, RP);
+            }
+            IRM_STAMP(5);
+            __syncthreads();
+            IRM_STAMP(0);
+            {  // y = Σ partials + Σ_{active rows} F_bot[n]·b[n]
+                const int cnt = list[N];
+                for (int e = tid; e < RP * 16; e += P.BT) {
+                    const int r = e >> 4, c = e & 15;
+                    float y = 0.f;
+                    for (int sp = 0; sp < P.nsplit; ++sp) y += Ypart[sp * RP * 16 + e];
+                    for (int j = 0; j < cnt; ++j) {
+                        const int nn = list[j];
+                        y += Fb[nn * RP + r] * Bs[nn * 16 + c];
+                    }
+                    if ((dirmask >> c) & 1u) Ydir[e] = y;
+                }
+            }
+            __syncthreads();
+            IRM_STAMP(1);
+            // Ymix = Ydir · JᵀJ  (per trajectory D×D)
+            for (int e = tid; e < RP * 16; e += P.BT) {
+                const int r = e >> 4, c = e & 15, tt = c / D, k = c - tt * D;
+                float y = 0.f;
+                if (tt < ntb) {
+#pragma unroll
+                    for (int d = 0; d < D; ++d) y += Ydir[r * 16 + tt * D + d] * P.JtJ[d * D + k];
+                }
+                Ymix[e] = y;
+            }
+            // BLS: partials of W = yᵀy (‖G‖_F and alpha_norm, optimizer_BLS.py:165-166)
+            if (bls && tvalid && needs_dir) {
+                float y[D];
+#pragma unroll
+                for (int d = 0; d < D; ++d) y[d] = (n < RP) ? Ydir[n * 16 + t * D + d] : 0.f;
+#pragma unroll
+                for (int a = 0; a < D; ++a)
+#pragma unroll
+                    for (int c = a; c < D; ++c) {
+                        const float w = wred_sum(y[a] * y[c]);
+                        if ((tid & 63) == 0) wp[wave * D * D + a * D + c] = w;
+                    }
+            }
+            __syncthreads();
+            IRM_STAMP(2);
+            // stage 2: dP = F(MP × RP) · Ymix, only the direction columns
+            mma_rows(F2, MT2, KQ2, Ymix, dP, dirmask, MP, wave, nwaves);
+            __syncthreads();
+            IRM_STAMP(3);
+            if (needs_dir) {
+                if (bls) {
+                    float W[D][D];
+#pragma unroll
+                    for (int a = 0; a < D; ++a)
+#pragma unroll
+                        for (int c = a; c < D; ++c) {
+                            float w = 0.f;
+                            for (int ww = 0; ww < WPT; ++ww) w += wp[(t * WPT + ww) * D * D + a * D + c];
+                            W[a][c] = w;
+                            W[c][a] = w;
+                        }
+                    // GᵀG = J W Jᵀ; ‖G‖² = tr; alpha_norm = Σ_ij (GᵀG)_ij / ‖G‖
+                    float tr = 0.f, all = 0.f;
+#pragma unroll
+                    for (int i = 0; i < D; ++i)
+#pragma unroll
+                        for (int j = 0; j < D; ++j) {
+                            float sacc = 0.f;
+#pragma unroll
+                            for (int a = 0; a < D; ++a) {
+                                float u = 0.f;
+#pragma unroll
+                                for (int c = 0; c < D; ++c) u += W[a][c] * P.J[j * D + c];
+                                sacc += P.J[i * D + a] * u;
+                            }
+                            if (i == j) tr += sacc;
+                            all += sacc;
+                        }
+                    gnorm = sqrtf(tr);
+                    anorm = all / gnorm;
+                    st.grad_evals++;  // inner-loop head: cost + grad at α (optimizer_BLS.py:163-164)
+                    st.cost_evals++;
+                    phase = PH_BLS_TRIAL;
+                    trial = 0;
+                } else {
+                    cfac = 1.f - P.lreg * lr;
+                    step = lr;
+                }
+                needs_dir = 0;
+            }
+        }
+        if (phase == PH_BLS_TRIAL) {
+            cfac = 1.f - P.lreg * lr;
+            step = lr / gnorm;
+        }
+        // ------------------------------------------------------- update
+        for (int e = tid; e < N; e += P.BT) act[e] = 0;
+        float q2[D], v2[D];
+        if (valid && (phase == PH_GD_INNER || phase == PH_BLS_TRIAL)) {
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                q2[k] = cfac * q[k] - step * dP[n * 16 + t * D + k];
+                v2[k] = cfac * v[k] - step * dP[(N + n) * 16 + t * D + k];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                q2[k] = q[k];
+                v2[k] = v[k];
+            }
+        }
+        // ------------------------------------------------------- evaluate
+        IRM_STAMP(6);
+        const bool ev = (phase != PH_DONE);  // wave-uniform
+        WP<D> w;
+        if (ev) {
+            if (valid) eval_waypoint<D>(P, q2, v2, obs, w);
+            IRM_STAMP(8);
+            eval_partials<D>(P, valid, w, n, wave, q2, v2, s, g, red, sg, t);
+        }
+        IRM_STAMP(9);
+        __syncthreads();
+        IRM_STAMP(7);
+        if (ev) {
+            const float lsg_e = lsg, ljl_e = ljl;
+            const EvalOut E = eval_finalize(P, red, sg, t, t * WPT, WPT, lsg_e, ljl_e);
+            // --------------------------------------------------- decide
+            int accept = 0;
+            bool snap = false, to_end = false;
+            const float nl = E.loss;
+            if (phase == PH_OUTER_START) {  // optimizer_GD.py:422-424 / optimizer_BLS.py:193
+                loss = nl;
+                if (!bls) st.cost_evals++;
+                accept = 2;
+                lr = bls ? P.bls_lr0 : P.gd_lr[outer];
+                needs_dir = 1;
+                if (!bls) phase = PH_GD_INNER;
+                if (P.max_inner <= 0) to_end = true;
+            } else if (phase == PH_GD_INNER) {  // optimizer_GD.py:394-408
+                st.grad_evals++;
+                st.cost_evals++;
+                if (loss - nl < P.llr) {
+                    to_end = true;  // minimized: the step is discarded
+                } else {
+                    accept = 1;
+                    loss = nl;
+                    inner++;
+                    st.inner_iterations++;
+                    snap = true;
+                    if (inner >= P.max_inner) to_end = true;
+                    else needs_dir = 1;
+                }
+            } else {  // PH_BLS_TRIAL: optimizer_BLS.py:136-150, 172-178
+                st.cost_evals++;
+                st.bls_trials++;
+                const float required = loss - P.bls_a * lr * anorm;
+                bool inner_end = false;
+                float improve = 0.f;
+                if (nl > required) {
+                    lr = lr * P.bls_bm;
+                    trial++;
+                    if (trial >= P.max_bls) inner_end = true;  // all rejected: new_loss = loss
+                } else {
+                    accept = 1;
+                    lr = lr * P.bls_bp;
+                    improve = loss - nl;
+                    loss = nl;
+                    inner_end = true;
+                }
+                if (inner_end) {
+                    if (improve < P.llr) {
+                        to_end = true;
+                    } else {
+                        inner++;
+                        st.inner_iterations++;
+                        snap = true;
+                        if (inner >= P.max_inner) to_end = true;
+                        else needs_dir = 1;
+                    }
+                }
+            }
+            if (accept) {
+                s_ds = E.ds;
+                s_dg = E.dg;
+                s_vs = E.vs;
+                s_vg = E.vg;
+                s_tmax = E.tmax;
+                s_tmin = E.tmin;
+                s_vabs = E.vabs;
+            }
+            if (to_end) {  // constraintsFulfilled (trajectory.py:129-137, robot.py:90-113)
+                const bool ok = s_ds < P.eps_p && s_dg < P.eps_p && s_vs < P.eps_v && s_vg < P.eps_v &&
+                                s_tmax <= P.pmax && s_tmin >= P.pmin && s_vabs <= P.vmax;
+                st.outer_iterations++;
+                st.constraints_ok = ok ? 1 : 0;
+                st.final_loss = loss;
+                needs_dir = 0;
+                if (ok) {
+                    phase = PH_DONE;
+                } else {
+                    outer++;
+                    lsg = lsg * P.lci;
+                    ljl = ljl * P.lci;
+                    inner = 0;
+                    phase = (outer >= P.max_outer) ? PH_DONE : PH_OUTER_START;
+                }
+            }
+            IRM_STAMP(10);
+            // --------------------------------------------------- gradient inputs at T2
+            if (valid) {
+                float a[D], bb[D];
+                grad_waypoint<D>(P, w, q2, v2, n, E.idx, lsg_e, ljl_e, s, g, a, bb);
+                bool any_b = false;
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    X[n * 16 + t * D + k] = a[k];
+                    Bs[n * 16 + t * D + k] = bb[k];
+                    any_b |= (bb[k] != 0.f);
+                }
+                if (any_b) act[n] = 1;
+            }
+            IRM_STAMP(12);
+            // --------------------------------------------------- accept
+            if (accept == 1) {
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    q[k] = q2[k];
+                    v[k] = v2[k];
+                }
+                cprod *= cfac;
+                for (int j = n; j < RP * D; j += NW) {  // y_acc ← c·y_acc + s·y  (α recovery)
+                    const int r = j / D, k = j - r * D;
+                    Yacc[r * 16 + t * D + k] = cfac * Yacc[r * 16 + t * D + k] + step * Ydir[r * 16 + t * D + k];
+                }
+            }
+            // extended-vis snapshot after every non-breaking inner iteration
+            // (optimizer_GD.py:366-367, optimizer_BLS.py:106-107)
+            if (rec && snap && st.series_len < P.max_series) {
+                if (valid) {
+#pragma unroll
+                    for (int k = 0; k < D; ++k)
+                        P.series[((b * P.max_series) + st.series_len) * N * D + n * D + k] = q[k];
+                }
+                st.series_len++;
+            }
+            if (n == 0) {
+                flags[t] = needs_dir;
+                flags[TB + t] = (phase == PH_DONE);
+            }
+        }
+        IRM_STAMP(15);
+        __syncthreads();
+        IRM_STAMP(11);
+        int alldone = 1;
+        for (int tt = 0; tt < ntb; ++tt) alldone &= flags[TB + tt];
+        if (alldone) break;
+    }
+
+    // ----------------------------------------------------------- epilogue
+    // α = cprod·α0 − (V_R·y_acc)·Jᵀ ; trajectory = T ; stats
+    mma_rows(P.Vfrag, NK / 16, RP / 16, Yacc, dP, 0xFFFFu, NK, wave, nwaves);
+    __syncthreads();
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            if (P.traj_out) P.traj_out[(b * N + n) * D + k] = q[k];
+            if (P.alpha_out) {
+                float acc = 0.f;
+#pragma unroll
+                for (int l = 0; l < D; ++l) acc += dP[n * 16 + t * D + l] * P.J[k * D + l];
+                P.alpha_out[(b * N + n) * D + k] = cprod * alpha0_at<D>(P, b, n, k) - acc;
+            }
+        }
+    }
+    if (P.stats && tvalid && n == 0) P.stats[b] = st;
+    IRM_STAMP(13);
+    if (tid == 0) prof.flush(P.prof);
+}
+
+// --------------------------------------------------- α-space eval kernels
+// mode 0: evaluate (K or dK)·α·J; 1: cost; 2: cost + grad; 3: constraints.
+// trajectory.py:63-65, 271-297, 129-180; same lane mapping as k_optimize.
+template <int D, int MAXT>
+__global__ __launch_bounds__(MAXT) void k_forward(KParams P, int mode) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const Plan L = plan_lds(P, false, false);
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nwaves = P.BT >> 6;
+    const int N = P.N, NW = P.NW, TB = P.TB, MP = P.MP, NK = P.NK;
+    const int WPT = NW >> 6;
+    const int t = wave / WPT;
+    const int n = tid - t * NW;
+    const int tb0 = blockIdx.x * TB;
+    const int ntb = min(TB, P.B - tb0);
+    if (ntb <= 0) return;
+    const bool tvalid = t < ntb;
+    const bool valid = tvalid && n < N;
+    const size_t b = (size_t)(tb0 + (tvalid ? t : 0));
+    float* XG = smem + L.X;
+    float* Pb = smem + L.dP;
+    float* red = smem + L.red;
+    float* sg = smem + L.sg;
+    float* obsL = smem + L.obs;
+
+    for (int e = tid; e < P.O * 2; e += P.BT) obsL[e] = P.obstacles[e];
+    stage_alpha<D>(P, tb0, ntb, XG, MP);
+    __syncthreads();
+    mma_rows(P.Lfrag, MP / 16, NK / 16, XG, Pb, 0xFFFFu, MP, wave, nwaves);
+    __syncthreads();
+    float q[D], v[D], s[D], g[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        float a = 0.f, c = 0.f;
+        if (valid) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                a += Pb[n * 16 + t * D + d] * P.J[d * D + k];
+                c += Pb[(N + n) * 16 + t * D + d] * P.J[d * D + k];
+            }
+        }
+        q[k] = a;
+        v[k] = c;
+        s[k] = tvalid ? P.start[b * D + k] : 0.f;
+        g[k] = tvalid ? P.goal[b * D + k] : 0.f;
+    }
+    if (mode == 0) {
+        if (valid) {
+#pragma unroll
+            for (int k = 0; k < D; ++k) P.out0[(b * N + n) * D + k] = P.which ? v[k] : q[k];
+        }
+        return;
+    }
+    for (int e = tid; e < MP * 16; e += P.BT) XG[e] = 0.f;
+    WP<D> w;
+    if (tvalid) {
+        if (valid) eval_waypoint<D>(P, q, v, obsL, w);
+        eval_partials<D>(P, valid, w, n, wave, q, v, s, g, red, sg, t);
+    }
+    __syncthreads();
+    EvalOut E{};
+    if (tvalid) E = eval_finalize(P, red, sg, t, t * WPT, WPT, P.lam_sg, P.lam_jl);
+    if (tvalid && n == 0) {
+        if (mode == 1 || mode == 2) {
+            if (P.out0) P.out0[b] = E.loss;
+        } else if (mode == 3) {
+            const bool f0 = E.ds < P.eps_p && E.dg < P.eps_p;
+            const bool f1 = E.vs < P.eps_v && E.vg < P.eps_v;
+            const bool f2 = E.tmax <= P.pmax && E.tmin >= P.pmin;
+            const bool f3 = E.vabs <= P.vmax;
+            if (P.out_ok) P.out_ok[b] = (f0 && f1 && f2 && f3) ? 1 : 0;
+            if (P.out0) {
+                float* r = P.out0 + b * 11;
+                r[0] = E.ds; r[1] = E.dg; r[2] = E.vs; r[3] = E.vg;
+                r[4] = E.tmax; r[5] = E.tmin; r[6] = E.vabs;
+                r[7] = f0; r[8] = f1; r[9] = f2; r[10] = f3;
+            }
+        }
+    }
+    if (mode != 2) return;
+    if (valid) {
+        float a[D], bb[D];
+        grad_waypoint<D>(P, w, q, v, n, E.idx, P.lam_sg, P.lam_jl, s, g, a, bb);
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            XG[n * 16 + t * D + k] = a[k];
+            XG[(N + n) * 16 + t * D + k] = bb[k];
+        }
+    }
+    __syncthreads();
+    // G = (Lᵀ·[a; b])·Jᵀ  (trajectory.py:295)
+    mma_rows(P.LTfrag, NK / 16, MP / 16, XG, Pb, 0xFFFFu, NK, wave, nwaves);
+    __syncthreads();
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            float acc = 0.f;
+#pragma unroll
+            for (int l = 0; l < D; ++l) acc += Pb[n * 16 + t * D + l] * P.J[k * D + l];
+            P.out1[(b * N + n) * D + k] = acc;
+        }
+    }
+}
+
+// ------------------------------------------- per-waypoint utility kernels
+// robot.py:29-36 + 75-87 for B×N waypoints.
+template <int D>
+__global__ void k_fk(KParams P, const float* traj, float* pos, float* jac) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int N = P.N;
+    if (i >= P.B * N) return;
+    const int b = i / N, n = i - b * N;
+    const float* q = traj + (size_t)i * D;
+    float cum = 0.f, fx = 0.f, fy = 0.f, Sx = 0.f, Sy = 0.f, xs[D], ys[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        cum += q[d];
+        float sn, cs;
+        sincosf(cum, &sn, &cs);
+        fx += P.link[d] * cs;
+        fy += P.link[d] * sn;
+        xs[d] = -(P.link[d] * sn);
+        ys[d] = P.link[d] * cs;
+        Sx += xs[d];
+        Sy += ys[d];
+    }
+    pos[(size_t)b * 2 * N + n] = fx;
+    pos[(size_t)b * 2 * N + N + n] = fy;
+    if (!jac) return;
+    float Cx = 0.f, Cy = 0.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        Cx += xs[d];
+        Cy += ys[d];
+        jac[(((size_t)b * 2 + 0) * N + n) * D + d] = (xs[d] + Sx) - Cx;
+        jac[(((size_t)b * 2 + 1) * N + n) * D + d] = (ys[d] + Sy) - Cy;
+    }
+}
+
+// environment.py:32-58 for B×N points (shared obstacles).
+__global__ void k_cost_vg(KParams P, const float* f, float* cv_out, float* cg_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int N = P.N;
+    if (i >= P.B * N) return;
+    const int b = i / N, n = i - b * N;
+    const float fx = f[(size_t)b * 2 * N + n], fy = f[(size_t)b * 2 * N + N + n];
+    float cv = 0.f, ax = 0.f, ay = 0.f;
+    for (int o = 0; o < P.O; ++o) {
+        const float dx = fx - P.obstacles[2 * o], dy = fy - P.obstacles[2 * o + 1];
+        const float r2 = dx * dx + dy * dy;
+        const float den = 0.5f + 0.5f * r2;
+        const float inv = __builtin_amdgcn_rcpf(den);
+        cv += 0.8f * inv;
+        const float i2 = inv * inv;
+        ax += (-0.8f * dx) * i2;
+        ay += (-0.8f * dy) * i2;
+    }
+    cv_out[i] = cv;
+    if (cg_out) {
+        cg_out[(size_t)b * 2 * N + n] = ax;
+        cg_out[(size_t)b * 2 * N + N + n] = ay;
+    }
+}
+
+// trajectory.py:73-78 batched: α0 = u⊗(s·J⁻¹) + w⊗(g·J⁻¹).
+__global__ void k_init_alpha(KParams P, float* alpha_out) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    const int N = P.N, D = P.D;
+    if (e >= P.B * N * D) return;
+    const int b = e / (N * D), r = e - b * N * D, n = r / D, d = r - n * D;
+    float sj = 0.f, gj = 0.f;
+    for (int k = 0; k < D; ++k) {
+        sj += P.start[(size_t)b * D + k] * P.Jinv[k * D + d];
+        gj += P.goal[(size_t)b * D + k] * P.Jinv[k * D + d];
+    }
+    alpha_out[e] = P.uvec[n] * sj + P.wvec[n] * gj;
+}
+
+// ------------------------------------------------------------- launchers
+template <class Fn>
+static hipError_t dispatch_d(int D, Fn&& fn) {
+    switch (D) {
+        case 1: return fn(std::integral_constant<int, 1>{});
+        case 2: return fn(std::integral_constant<int, 2>{});
+        case 3: return fn(std::integral_constant<int, 3>{});
+        case 4: return fn(std::integral_constant<int, 4>{});
+        case 5: return fn(std::integral_constant<int, 5>{});
+        case 6: return fn(std::integral_constant<int, 6>{});
+        case 7: return fn(std::integral_constant<int, 7>{});
+        case 8: return fn(std::integral_constant<int, 8>{});
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <class Fn>
+static hipError_t dispatch_t(int BT, Fn&& fn) {
+    if (BT <= 256) return fn(std::integral_constant<int, 256>{});
+    if (BT <= 512) return fn(std::integral_constant<int, 512>{});
+    if (BT <= 1024) return fn(std::integral_constant<int, 1024>{});
+    return hipErrorInvalidValue;
+}
+
+template <class K, class... Args>
+static hipError_t launch_lds(K kernel, int grid, int threads, size_t lds, hipStream_t s, Args... args) {
+    hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), lds, s, args...);
+    return hipGetLastError();
+}
+
+hipError_t launch_optimize(const KParams& p, hipStream_t s) {
+    const bool stage = p.ops_in_lds != 0;
+    const Plan L = plan_lds(p, stage, true);
+    const size_t lds = (size_t)L.total * 4;
+    const int grid = (p.B + p.TB - 1) / p.TB;
+    if (grid <= 0) return hipSuccess;
+    return dispatch_d(p.D, [&](auto dc) {
+        constexpr int DD = decltype(dc)::value;
+        return dispatch_t(p.BT, [&](auto tc) {
+            constexpr int TT = decltype(tc)::value;
+            return stage ? launch_lds(k_optimize<DD, TT, true>, grid, p.BT, lds, s, p)
+                         : launch_lds(k_optimize<DD, TT, false>, grid, p.BT, lds, s, p);
+        });
+    });
+}
+
+hipError_t launch_forward(const KParams& p, int mode, hipStream_t s) {
+    const Plan L = plan_lds(p, false, false);
+    const size_t lds = (size_t)L.total * 4;
+    const int grid = (p.B + p.TB - 1) / p.TB;
+    if (grid <= 0) return hipSuccess;
+    return dispatch_d(p.D, [&](auto dc) {
+        constexpr int DD = decltype(dc)::value;
+        return dispatch_t(p.BT, [&](auto tc) {
+            constexpr int TT = decltype(tc)::value;
+            return launch_lds(k_forward<DD, TT>, grid, p.BT, lds, s, p, mode);
+        });
+    });
+}
+
+hipError_t launch_fk(const KParams& p, const float* traj, float* pos, float* jac, hipStream_t s) {
+    const int n = p.B * p.N;
+    if (n <= 0) return hipSuccess;
+    return dispatch_d(p.D, [&](auto dc) {
+        constexpr int DD = decltype(dc)::value;
+        hipLaunchKernelGGL(k_fk<DD>, dim3((n + 255) / 256), dim3(256), 0, s, p, traj, pos, jac);
+        return hipGetLastError();
+    });
+}
+
+hipError_t launch_cost_vg(const KParams& p, const float* f, float* cv, float* cg, hipStream_t s) {
+    const int n = p.B * p.N;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_cost_vg, dim3((n + 255) / 256), dim3(256), 0, s, p, f, cv, cg);
+    return hipGetLastError();
+}
+
+hipError_t launch_init_alpha(const KParams& p, float* alpha_out, hipStream_t s) {
+    const int n = p.B * p.N * p.D;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_init_alpha, dim3((n + 255) / 256), dim3(256), 0, s, p, alpha_out);
+    return hipGetLastError();
+}
+
+}  // namespace irm

@@ -1,0 +1,108 @@
+// irm_kernels.hpp — launch-side interface between the C-ABI host code
+// (irm_host.cpp) and the gfx950 kernels (irm_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/irm.h"
+
+namespace irm {
+
+constexpr int kCols = 16;         // MFMA 16x16x4 column tile = TB·D columns
+constexpr int kMaxThreads = 1024; // one lane per (trajectory, waypoint): TB·NW ≤ 1024
+
+// Per-trajectory phases of the on-device optimiser state machine.
+enum Phase : int32_t { PH_OUTER_START = 0, PH_GD_INNER = 1, PH_BLS_TRIAL = 2, PH_DONE = 3 };
+
+// Everything a kernel needs, passed by value (kernarg segment).
+struct KParams {
+    // shapes
+    int32_t N, D, R, TB, B, O, obs_stride;
+    int32_t NK;   // N rounded up to 16 (k extent of N-contractions)
+    int32_t MP;   // 2N rounded up to 16 (rows of [K;dK])
+    int32_t RP;   // R (multiple of 16)
+    int32_t ops_in_lds;  // operator fragments staged into LDS
+    int32_t NW;          // lanes per trajectory = N rounded up to 64 (whole waves)
+    int32_t BT;          // threads per workgroup = TB·NW
+    int32_t nsplit;      // stage-1 split-K factor
+    // optimiser
+    int32_t optimizer, max_inner, max_outer, max_bls, cvdl, record_series, max_series, pad0;
+    float llr, lci, lsg0, ljl0, eps_p, eps_v, lmax, lreg;
+    float bls_lr0, bls_a, bls_bp, bls_bm, vmax, pmax, pmin, pad1;
+    // derived fp32 constants (reference casts its Python doubles to fp32)
+    float mean_pos, std_pos, std2, vmax2, thr_hi, thr_lo, thr_v, invN;
+    float inv_std_pos, inv_vmax, inv_std2, inv_vmax2;  // reciprocals: x/c → x·(1/c) in the hot loops
+    uint32_t Nmagic, NDmagic;  // ⌈2³²/N⌉, ⌈2³²/(N·D)⌉: exact __umulhi division for dividends < 2¹⁶
+    float gd_lr[IRM_MAX_LR];
+    float link[IRM_MAX_JOINTS];
+    float J[IRM_MAX_JOINTS * IRM_MAX_JOINTS];    // J (D×D, row-major, stride D)
+    float JtJ[IRM_MAX_JOINTS * IRM_MAX_JOINTS];  // JᵀJ
+    float Jinv[IRM_MAX_JOINTS * IRM_MAX_JOINTS]; // J⁻¹
+    // operators (device, fp32)
+    const float* Lfrag;   // A-fragments of L = [K;dK]   (MP × NK)
+    const float* LTfrag;  // A-fragments of Lᵀ           (NK × MP)
+    const float* F1frag;  // A-fragments of F_topᵀ        (RP × NK)
+    const float* F2frag;  // A-fragments of F             (MP × RP)
+    const float* Fbot;    // F rows N..2N-1, row-major    (N × RP)
+    const float* Vr;      // V_R, row-major               (N × RP)
+    const float* Vfrag;   // A-fragments of V_R           (NK × RP)
+    const float* uvec;    // K⁻¹(1-c)   (N)  initTrajectory basis
+    const float* wvec;    // K⁻¹c       (N)
+    // batch I/O
+    const float* alpha0;
+    const float* start;
+    const float* goal;
+    const float* obstacles;
+    float* alpha_out;
+    float* traj_out;
+    irm_stats* stats;
+    float* series;
+    // cost weights of the current call (optimiser: lam_max = --lambda-max-cost)
+    float lam_sg, lam_jl, lam_max, one_m_lmax;  // one_m_lmax = fp32(1 − λmax in double)
+    int32_t which, pad2;
+    float* out0;   // evaluate: B×N×D; cost: B; constraints report: B×11
+    float* out1;   // grad: B×N×D
+    uint8_t* out_ok;
+    unsigned long long* prof;  // IRM_PHASE_PROFILE builds: per-block phase cycle counters
+};
+
+constexpr int kProfPhases = 16;
+
+// Operator fragment sizes (floats) for the layout of mfma_frag_index.
+__host__ __device__ inline int64_t frag_floats(int M, int K) {
+    int MT = (M + 15) / 16, KQ = (K + 15) / 16;
+    return (int64_t)MT * KQ * 64 * 4;
+}
+
+// Element (row, k) of a row-major M×K matrix in the 16x16x4 A-fragment layout:
+// block (row/16, k/16), lane = row%16 + 16*(k%4), float slot j = (k%16)/4.
+__host__ __device__ inline int64_t frag_index(int row, int k, int K) {
+    int KQ = (K + 15) / 16;
+    int mt = row / 16, kq = k / 16, kk = k % 16;
+    int lane = (row % 16) + 16 * (kk % 4), j = kk / 4;
+    return (((int64_t)mt * KQ + kq) * 64 + lane) * 4 + j;
+}
+
+// LDS layout of the optimiser / eval workgroups (float offsets, 16-B aligned).
+struct Plan {
+    int f1, f2, fb;              // staged operators F_topᵀ, F, F_bot (optimiser, ops_in_lds)
+    int X, Bs;                   // MFMA B operand: a (NK × 16) and b (N × 16) / [a; b] (MP × 16)
+    int dP;                      // MFMA output rows (MP × 16)
+    int Ypart, Ydir, Ymix, Yacc; // stage-1 partials, y, y·JᵀJ, Σ steps·y
+    int red, sg, wp;             // wave partials, start/goal rows, BLS Gram partials
+    int flags, act, list;        // per-trajectory flags, active sparse rows
+    int obs;                     // obstacles (shared or per trajectory)
+    int total;
+};
+
+__host__ __device__ Plan plan_lds(const KParams& p, bool ops_lds, bool optimizer);
+
+// launchers (return hipError_t)
+hipError_t launch_init_alpha(const KParams& p, float* alpha_out, hipStream_t s);
+hipError_t launch_optimize(const KParams& p, hipStream_t s);
+hipError_t launch_forward(const KParams& p, int mode, hipStream_t s);  // mode: 0 evaluate, 1 cost, 2 cost+grad, 3 constraints
+hipError_t launch_fk(const KParams& p, const float* traj, float* pos, float* jac, hipStream_t s);
+hipError_t launch_cost_vg(const KParams& p, const float* f, float* cv, float* cg, hipStream_t s);
+
+}  // namespace irm

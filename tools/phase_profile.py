@@ -1,0 +1,49 @@
+"""Developer diagnostic: per-phase cycle breakdown of k_optimize.
+
+Needs the IRM_PHASE_PROFILE build (python -m irm_motion_planning_amd.build --prof);
+run with IRM_LIB=<repo>/irm_motion_planning_amd/libirm_hip_prof.so on the GPU box.
+"""
+import ctypes
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import bench  # noqa: E402
+from irm_motion_planning_amd.context import Context  # noqa: E402
+from irm_motion_planning_amd.params import params_from_args  # noqa: E402
+
+PHASES = ["dir:stage1 barrier-wait", "dir:reduce+sparse", "dir:W+mix", "dir:stage2", "round-top (flags)",
+          "dir:stage1 mfma (w0)", "post-dir + update", "E1 barrier-wait", "eval_waypoint", "eval_partials",
+          "finalize+decide", "end barrier-wait", "grad_waypoint+store", "epilogue", "prologue", "accept+yacc+flags"]
+
+
+def run(cfg, tb=0, rank=0, faithful=False):
+    args = bench.make_args(cfg, faithful, 200)
+    start, goal, obstacles = bench.make_problem(cfg, 1, 0)
+    ctx = Context(params_from_args(args, traj_per_block=tb, operator_rank=rank))
+    info = ctx.info()
+    ctx.optimize(start, goal, obstacles)
+    t0 = time.perf_counter()
+    alpha, traj, st = ctx.optimize(start, goal, obstacles)
+    dt = time.perf_counter() - t0
+    nb = 4096
+    buf = (ctypes.c_uint64 * (nb * 16))()
+    n = ctx.lib.irm_debug_phase_profile(ctx.handle, buf, nb)
+    prof = np.frombuffer(buf, dtype=np.uint64, count=n * 16).reshape(n, 16).astype(np.float64)
+    rounds = float(np.max(st["grad_evals"]) + np.max(st["outer_iterations"]))
+    tot = prof.sum(1)
+    print(f"== {cfg} tb={info['traj_per_block']} R={info['operator_rank']} blocks={n} host {1000*dt:.2f} ms "
+          f"rounds~{rounds:.0f} total cycles/block mean {tot.mean():.0f} -> {tot.mean()/rounds:.0f} per round")
+    for i, name in enumerate(PHASES):
+        c = prof[:, i].mean()
+        if c > 0:
+            print(f"   {name:22s} {c/rounds:9.0f} cyc/round  ({100*c/tot.mean():5.1f} %)")
+
+
+if __name__ == "__main__":
+    for cfg in sys.argv[1:] or ["c3", "c2", "c5"]:
+        run(cfg)
