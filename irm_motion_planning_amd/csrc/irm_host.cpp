@@ -219,9 +219,10 @@ int choose_shape(const irm_ctx* c, int B, bool optimizer, KParams& kp, int* lds_
     for (; tb >= 1; --tb) {
         kp.TB = tb;
         kp.BT = tb * kp.NW;
-        const int nw = kp.BT / 64, MT1 = kp.RP / 16, KQ1 = kp.NK / 16;
+        const int nw = kp.BT / 64, MT1 = kp.RP / 16, KQ1 = kp.MP / 16;
         kp.nsplit = std::max(1, std::min(KQ1, nw / std::max(1, MT1)));
         if (optimizer) {
+            kp.regops = irm::regops_fit(kp) ? 1 : 0;
             irm::Plan a = irm::plan_lds(kp, true, true);
             if ((size_t)a.total * 4 <= lds_cap) {
                 kp.ops_in_lds = 1;
@@ -231,6 +232,7 @@ int choose_shape(const irm_ctx* c, int B, bool optimizer, KParams& kp, int* lds_
             irm::Plan b = irm::plan_lds(kp, false, true);
             if ((size_t)b.total * 4 <= lds_cap) {
                 kp.ops_in_lds = 0;
+                kp.regops = 0;
                 if (lds_bytes_out) *lds_bytes_out = b.total * 4;
                 return tb;
             }
@@ -450,10 +452,10 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
         for (int j = 0; j < N; ++j) A[(size_t)j * MP + m] = Ld[(size_t)m * N + j];
     fill_frag(frag, NK, MP, A);
     rc |= upload(&c->d_LTfrag, frag);
-    A.assign((size_t)RP * NK, 0.0);  // F_topᵀ (RP × NK)
-    for (int n = 0; n < N; ++n)
-        for (int r = 0; r < RP; ++r) A[(size_t)r * NK + n] = F[(size_t)n * RP + r];
-    fill_frag(frag, RP, NK, A);
+    A.assign((size_t)RP * MP, 0.0);  // Fᵀ (RP × MP): stage 1 contracts y = Fᵀ·[a; b]
+    for (int m = 0; m < 2 * N; ++m)
+        for (int r = 0; r < RP; ++r) A[(size_t)r * MP + m] = F[(size_t)m * RP + r];
+    fill_frag(frag, RP, MP, A);
     rc |= upload(&c->d_F1, frag);
     A.assign((size_t)MP * RP, 0.0);  // F (MP × RP)
     for (int m = 0; m < 2 * N; ++m)
@@ -561,6 +563,11 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
         if (!lu_solve_f32(D, p->jac, eye.data(), D, Jinv.data())) {
             irm_ctx_destroy(c);
             return fail(IRM_EINVAL, "J is singular");
+        }
+        for (int a = 0; a < D; ++a) {
+            double u = 0.0;
+            for (int i = 0; i < D; ++i) u += (double)p->jac[(size_t)i * D + a];
+            kp.Jcol[a] = (float)u;
         }
         for (int i = 0; i < D * D; ++i) {
             kp.J[i] = p->jac[i];

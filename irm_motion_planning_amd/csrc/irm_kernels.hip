@@ -44,34 +44,27 @@ __host__ __device__ Plan plan_lds(const KParams& p, bool ops_lds, bool optimizer
     };
     const int N = p.N, TB = p.TB, nw = p.BT / 64;
     L.f1 = L.f2 = L.fb = 0;
-    if (optimizer && ops_lds) {
-        L.f1 = take((int)frag_floats(p.RP, p.NK));
+    if (optimizer && ops_lds && !p.regops) {  // with REGOPS the A-fragments live in VGPRs
+        L.f1 = take((int)frag_floats(p.RP, p.MP));
         L.f2 = take((int)frag_floats(p.MP, p.RP));
-        L.fb = take(N * p.RP);
     }
+    L.X = take(p.MP * kLd);  // [a; b] stacked: rows 0..N-1 = a, N..2N-1 = b
+    L.Bs = L.X + N * kLd;
+    L.dP = take(p.MP * kLd);
+    L.Ydir = L.Yacc = 0;
     if (optimizer) {
-        L.X = take(p.NK * kCols);
-        L.Bs = take(N * kCols);
+        L.Ypart = take(p.nsplit * p.RP * kLd);
+        L.Ymix = take(p.RP * kLd);
     } else {
-        L.X = take(p.MP * kCols);  // [a; b] stacked (rows 0..N-1, N..2N-1)
-        L.Bs = L.X + N * kCols;
+        L.Ypart = L.Ymix = 0;
     }
-    L.dP = take(p.MP * kCols);
-    if (optimizer) {
-        L.Ypart = take(p.nsplit * p.RP * kCols);
-        L.Ydir = take(p.RP * kCols);
-        L.Ymix = take(p.RP * kCols);
-        L.Yacc = take(p.RP * kCols);
-    } else {
-        L.Ypart = L.Ydir = L.Ymix = L.Yacc = 0;
-    }
+    L.alist = L.acnt = 0;
     L.red = take(nw * 10);
     L.sg = take(TB * 4);
-    L.wp = take(nw * p.D * p.D);
-    L.flags = take(2 * TB);
-    L.act = take(N + 4);
-    L.list = take(N + 4);
-    L.obs = take((p.obs_stride ? TB : 1) * p.O * 2 + 4);
+    L.wp = take(nw * 2);
+    L.flags = take(4);
+    L.act = L.list = 0;
+    L.obs = take((p.obs_stride ? TB : 1) * ((p.O + 3) & ~3) * 2 + 4);
     L.total = off;
     return L;
 }
@@ -173,21 +166,21 @@ struct Prof {
 // ---------------------------------------------------------- MFMA contraction
 // acc(16×16 tile) = Σ_{kq∈[kq0,kq1)} A[tile, kq] · X[16kq .. 16kq+15][0..15]
 // A: 16x16x4 A-fragments (frag_index layout), one float4 per lane = 4 k-steps.
-// X: LDS, row stride 16 floats (one row per k); lane l reads row 4j+(l>>4),
-// column l&15 of each k-step: 64 consecutive floats, conflict-free.
+// X: LDS, row stride kLd floats (one row per k); lane l reads row 4j+(l>>4),
+// column l&15 of each k-step.
 __device__ __forceinline__ f32x4 mma_tile(const float* __restrict__ A, int KQ, int tile, int kq0, int kq1,
                                           const float* __restrict__ X) {
     const int lane = threadIdx.x & 63;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    const float* xl = X + (lane >> 4) * 16 + (lane & 15);
+    const float* xl = X + (lane >> 4) * kLd + (lane & 15);
     const f32x4* ap = reinterpret_cast<const f32x4*>(A) + ((size_t)tile * KQ) * 64 + lane;
     for (int kq = kq0; kq < kq1; ++kq) {
         f32x4 a = ap[(size_t)kq * 64];
-        const float* xb = xl + kq * 256;
+        const float* xb = xl + kq * 16 * kLd;
         acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], xb[0], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], xb[64], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], xb[128], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], xb[192], acc1, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], xb[4 * kLd], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], xb[8 * kLd], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], xb[12 * kLd], acc1, 0, 0, 0);
     }
     return acc0 + acc1;
 }
@@ -200,7 +193,7 @@ __device__ __forceinline__ void store_tile(float* out, int tile, f32x4 acc, unsi
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         int row = tile * 16 + 4 * (lane >> 4) + i;
-        if (row < rows) out[row * 16 + col] = acc[i];
+        if (row < rows) out[row * kLd + col] = acc[i];
     }
 }
 
@@ -214,6 +207,29 @@ __device__ void mma_rows(const float* A, int MT, int KQ, const float* X, float* 
 }
 
 // ------------------------------------------------ per-waypoint physics
+// sin/cos for robot.py's joint angles: Cody-Waite reduction by π/2 (3-part
+// split, fma) and the cephes single-precision minimax polynomials on
+// [−π/4, π/4]; ≈1 ulp, branch-free.  |x| > 1e4 rad falls back to sincosf.
+__device__ __forceinline__ void sincos_fast(float x, float& sn, float& cs) {
+    if (__builtin_expect(fabsf(x) > 1.0e4f, 0)) {
+        sincosf(x, &sn, &cs);
+        return;
+    }
+    const float kf = rintf(x * 0.636619772f);
+    float r = fmaf(kf, -1.57079637050628662109375f, x);
+    r = fmaf(kf, 4.371138828673793e-08f, r);
+    r = fmaf(kf, 1.7151245100058819e-15f, r);
+    const float z = r * r;
+    const float sp = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
+    const float cp = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f), 4.166664568298827e-2f),
+                          fmaf(-0.5f, z, 1.0f));
+    const int q = (int)kf & 3;
+    const float s0 = (q & 1) ? cp : sp;
+    const float c0 = (q & 1) ? sp : cp;
+    sn = (q & 2) ? -s0 : s0;
+    cs = ((q + 1) & 2) ? -c0 : c0;
+}
+
 template <int D>
 struct WP {
     float cv, gx, gy;        // obstacle potential and its gradient at the end effector
@@ -233,7 +249,7 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
     for (int d = 0; d < D; ++d) {
         cum += q[d];
         float sn, cs;
-        sincosf(cum, &sn, &cs);
+        sincos_fast(cum, sn, cs);
         fx += P.link[d] * cs;
         fy += P.link[d] * sn;
         xs[d] = -(P.link[d] * sn);
@@ -249,9 +265,11 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
         w.jx[d] = (xs[d] + Sx) - Cx;
         w.jy[d] = (ys[d] + Sy) - Cy;
     }
+    // Obstacles are staged in LDS padded to a multiple of 4 with sentinels at
+    // (1e20, 1e20): r² overflows to +inf, rcp → 0, so a sentinel adds exactly 0.
     float cv = 0.f, ax = 0.f, ay = 0.f;
-    for (int o = 0; o < P.O; ++o) {
-        const float dx = fx - ob[2 * o], dy = fy - ob[2 * o + 1];
+    auto pair = [&](float ox, float oy) {
+        const float dx = fx - ox, dy = fy - oy;
         const float r2 = dx * dx + dy * dy;
         const float den = 0.5f + 0.5f * r2;
         const float inv = __builtin_amdgcn_rcpf(den);
@@ -259,6 +277,15 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
         const float i2 = inv * inv;
         ax += (-0.8f * dx) * i2;
         ay += (-0.8f * dy) * i2;
+    };
+    const f32x4* o4 = reinterpret_cast<const f32x4*>(ob);
+    const int nq = (P.O + 3) >> 2;
+    for (int c = 0; c < nq; ++c) {
+        const f32x4 p0 = o4[2 * c], p1 = o4[2 * c + 1];
+        pair(p0[0], p0[1]);
+        pair(p0[2], p0[3]);
+        pair(p1[0], p1[1]);
+        pair(p1[2], p1[3]);
     }
     w.cv = cv;
     w.gx = ax;
@@ -395,12 +422,29 @@ __device__ __forceinline__ EvalOut eval_finalize(const KParams& P, const float* 
     return e;
 }
 
+// Obstacles into LDS: one shared set (obs_stride 0) or one per trajectory,
+// each padded to obs_pitch floats with zero-contribution sentinels.
+__host__ __device__ inline int obs_pitch(int O) { return ((O + 3) & ~3) * 2; }
+__device__ void stage_obstacles(const KParams& P, int tb0, int ntb, float* obsL) {
+    const int pitch = obs_pitch(P.O), nsets = P.obs_stride ? P.TB : 1;
+    for (int e = threadIdx.x; e < nsets * pitch; e += P.BT) {
+        const int tt = e / pitch, r = e - tt * pitch;
+        float val = 1.0e20f;
+        if (r < P.O * 2) {
+            if (!P.obs_stride) val = P.obstacles[r];
+            else if (tt < ntb) val = P.obstacles[(size_t)(tb0 + tt) * P.obs_stride + r];
+        }
+        obsL[e] = val;
+    }
+}
+
 // α0 of the block's trajectories into X[n][tD+d] (rows ≥ N / unused columns 0).
 template <int D>
 __device__ void stage_alpha(const KParams& P, int tb0, int ntb, float* X, int xrows) {
     const int N = P.N;
     for (int e = threadIdx.x; e < xrows * 16; e += P.BT) {
         const int n = e >> 4, c = e & 15, t = c / D, d = c - t * D;
+        float* dst = X + n * kLd + c;
         float val = 0.f;
         if (n < N && t < ntb) {
             const size_t b = (size_t)(tb0 + t);
@@ -415,7 +459,7 @@ __device__ void stage_alpha(const KParams& P, int tb0, int ntb, float* X, int xr
                 val = P.uvec[n] * sj + P.wvec[n] * gj;
             }
         }
-        X[e] = val;
+        *dst = val;
     }
 }
 
@@ -431,22 +475,80 @@ __device__ __forceinline__ float alpha0_at(const KParams& P, size_t b, int n, in
 }
 
 // ------------------------------------------------------------ optimiser
-template <int D, int MAXT, bool OPS_LDS>
+// Interleaved wave reduction of one evaluation's per-waypoint terms.
+// usum: Σ_n [(1−λmax)/N·cost_v[n] + λjl/N·(jp[n] + jv[n])], the mean-obstacle and
+// joint-limit terms of trajectory.py:281 folded into one sum.
+struct EvalRed {
+    float cmax;
+    int cidx;
+    float usum, tx, tn, va;
+};
+template <int C>
+__device__ __forceinline__ void ered_step(EvalRed& r) {
+    const float ov = dppf<C>(r.cmax);
+    const int oi = dppi<C>(r.cidx);
+    const float s1 = dppf<C>(r.usum);
+    const float m1 = dppf<C>(r.tx), m2 = dppf<C>(r.tn), m3 = dppf<C>(r.va);
+    amax_step(r.cmax, r.cidx, ov, oi);
+    r.usum += s1;
+    r.tx = fmaxf(r.tx, m1);
+    r.tn = fminf(r.tn, m2);
+    r.va = fmaxf(r.va, m3);
+}
+// Reduce within the wave; lane 0 stores the partial record at red[wave].
+__device__ __forceinline__ void ered_store(EvalRed r, float* red, int wave) {
+    ered_step<0xB1>(r);
+    ered_step<0x4E>(r);
+    ered_step<0x141>(r);
+    ered_step<0x140>(r);
+    EvalRed o;
+    o.cmax = lanef(r.cmax, 0);
+    o.cidx = __builtin_amdgcn_readlane(r.cidx, 0);
+    o.usum = lanef(r.usum, 0);
+    o.tx = lanef(r.tx, 0);
+    o.tn = lanef(r.tn, 0);
+    o.va = lanef(r.va, 0);
+#pragma unroll
+    for (int l = 16; l < 64; l += 16) {
+        amax_step(o.cmax, o.cidx, lanef(r.cmax, l), __builtin_amdgcn_readlane(r.cidx, l));
+        o.usum += lanef(r.usum, l);
+        o.tx = fmaxf(o.tx, lanef(r.tx, l));
+        o.tn = fminf(o.tn, lanef(r.tn, l));
+        o.va = fmaxf(o.va, lanef(r.va, l));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        float* q = red + wave * 10;
+        q[0] = o.cmax;
+        q[1] = __int_as_float(o.cidx);
+        q[2] = o.usum;
+        q[3] = o.tx;
+        q[4] = o.tn;
+        q[5] = o.va;
+    }
+}
+
+// Operator fragments a wave keeps in VGPRs across all rounds (REGOPS).
+constexpr int kS1Q(int maxt) { return maxt <= 256 ? 8 : 4; }   // stage-1 float4 per wave
+constexpr int kS2T(int maxt) { return maxt <= 256 ? 8 : 4; }   // stage-2 tiles per wave (KQ2 ≤ 2)
+
+template <int D, int MAXT, bool OPS_LDS, bool REGOPS>
 __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
+    constexpr int S1Q = kS1Q(MAXT), S2T = kS2T(MAXT);
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const Plan L = plan_lds(P, OPS_LDS, true);
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nwaves = P.BT >> 6;
     const int N = P.N, NW = P.NW, TB = P.TB, RP = P.RP, MP = P.MP, NK = P.NK;
     const int WPT = NW >> 6;            // waves per trajectory
     const int t = wave / WPT;           // this lane's trajectory (wave-uniform)
-    const int n = tid - t * NW;         // this lane's waypoint
+    const int n = tid - t * NW;         // this lane's waypoint (and row r of y for n < RP)
     const int tb0 = blockIdx.x * TB;
     const int ntb = min(TB, P.B - tb0);
     if (ntb <= 0) return;
     const bool tvalid = t < ntb;
     const bool valid = tvalid && n < N;
+    const bool yrow = tvalid && n < RP;
     const size_t b = (size_t)(tb0 + (tvalid ? t : 0));
     const bool bls = (P.optimizer == IRM_OPT_BLS);
     const bool rec = P.record_series && P.series;
@@ -457,72 +559,69 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
     float* Bs = smem + L.Bs;
     float* dP = smem + L.dP;
     float* Ypart = smem + L.Ypart;
-    float* Ydir = smem + L.Ydir;
     float* Ymix = smem + L.Ymix;
-    float* Yacc = smem + L.Yacc;
     float* red = smem + L.red;
     float* sg = smem + L.sg;
     float* wp = smem + L.wp;
-    int* flags = reinterpret_cast<int*>(smem + L.flags);
-    int* act = reinterpret_cast<int*>(smem + L.act);
-    int* list = reinterpret_cast<int*>(smem + L.list);
+    unsigned* flagw = reinterpret_cast<unsigned*>(smem + L.flags);  // [0,1] dir masks, [2] done mask
     float* obsL = smem + L.obs;
     const float* F1 = P.F1frag;
     const float* F2 = P.F2frag;
-    const float* Fb = P.Fbot;
 
-    const int KQ1 = NK / 16, MT1 = RP / 16;   // stage 1: (RP × NK)·(NK × 16)
+    const int KQ1 = MP / 16, MT1 = RP / 16;   // stage 1: (RP × MP)·(MP × 16), K over [a; b]
     const int KQ2 = RP / 16, MT2 = MP / 16;   // stage 2: (MP × RP)·(RP × 16)
+    const int nsplit = P.nsplit;
+    // stage-1 unit of this wave (split-K): tile u1 % MT1, k-quads [kq0, kq1)
+    const bool has1 = wave < MT1 * nsplit;
+    const int tile1 = wave % MT1, sp1 = wave / MT1;
+    const int kq0 = (KQ1 * sp1) / nsplit, kq1 = (KQ1 * (sp1 + 1)) / nsplit;
 
     // ----------------------------------------------------------- prologue
-    if (OPS_LDS) {
-        const int n1 = (int)frag_floats(RP, NK) / 4, n2 = (int)frag_floats(MP, RP) / 4, n3 = N * RP / 4;
+    if (OPS_LDS && !REGOPS) {
+        const int n1 = (int)frag_floats(RP, MP) / 4, n2 = (int)frag_floats(MP, RP) / 4;
         const f32x4* g1 = reinterpret_cast<const f32x4*>(P.F1frag);
         const f32x4* g2 = reinterpret_cast<const f32x4*>(P.F2frag);
-        const f32x4* g3 = reinterpret_cast<const f32x4*>(P.Fbot);
         f32x4* l1 = reinterpret_cast<f32x4*>(smem + L.f1);
         f32x4* l2 = reinterpret_cast<f32x4*>(smem + L.f2);
-        f32x4* l3 = reinterpret_cast<f32x4*>(smem + L.fb);
         for (int e = tid; e < n1; e += P.BT) l1[e] = g1[e];
         for (int e = tid; e < n2; e += P.BT) l2[e] = g2[e];
-        for (int e = tid; e < n3; e += P.BT) l3[e] = g3[e];
         F1 = smem + L.f1;
         F2 = smem + L.f2;
-        Fb = smem + L.fb;
     }
-    {
-        const int nobs = (P.obs_stride ? TB : 1) * P.O * 2;
-        for (int e = tid; e < nobs; e += P.BT) {
-            float val = 0.f;
-            if (P.obs_stride) {
-                const int tt = e / (P.O * 2), r = e - tt * P.O * 2;
-                if (tt < ntb) val = P.obstacles[(size_t)(tb0 + tt) * P.obs_stride + r];
-            } else {
-                val = P.obstacles[e];
-            }
-            obsL[e] = val;
+    f32x4 a1[REGOPS ? S1Q : 1], a2[REGOPS ? S2T * 2 : 1];
+    if (REGOPS) {  // operator A-fragments resident in VGPRs for the whole launch
+        const f32x4* g1 = reinterpret_cast<const f32x4*>(P.F1frag);
+        const f32x4* g2 = reinterpret_cast<const f32x4*>(P.F2frag);
+#pragma unroll
+        for (int i = 0; i < S1Q; ++i) {
+            a1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (has1 && kq0 + i < kq1) a1[i] = g1[((size_t)tile1 * KQ1 + kq0 + i) * 64 + lane];
         }
+#pragma unroll
+        for (int j = 0; j < S2T; ++j)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                a2[j * 2 + i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                const int tile = wave + j * nwaves;
+                if (tile < MT2 && i < KQ2) a2[j * 2 + i] = g2[((size_t)tile * KQ2 + i) * 64 + lane];
+            }
     }
-    for (int e = tid; e < N * 16; e += P.BT) Bs[e] = 0.f;
-    for (int e = tid; e < RP * 16; e += P.BT) {
-        Ydir[e] = 0.f;
-        Ymix[e] = 0.f;
-        Yacc[e] = 0.f;
-    }
-    for (int e = tid; e < N; e += P.BT) act[e] = 0;
-    if (tid < TB) {
-        flags[tid] = 0;                          // needs a direction next round
-        flags[TB + tid] = (tid < ntb) ? 0 : 1;   // done
+    stage_obstacles(P, tb0, ntb, obsL);
+    for (int e = tid; e < RP * kLd; e += P.BT) Ymix[e] = 0.f;
+    if (tid == 0) {
+        flagw[0] = flagw[1] = 0u;
+        flagw[2] = 0u;
     }
     stage_alpha<D>(P, tb0, ntb, X, NK);
     __syncthreads();
     // T0 = (K·α0)·J, V0 = (dK·α0)·J  (trajectory.py:63-65)
-    mma_rows(P.Lfrag, MT2, KQ1, X, dP, 0xFFFFu, MP, wave, nwaves);
+    mma_rows(P.Lfrag, MT2, NK / 16, X, dP, 0xFFFFu, MP, wave, nwaves);
     __syncthreads();
-    float q[D], v[D], s[D], g[D];
+    float q[D], v[D], s[D], g[D], ydir[D], yacc[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) {
         q[k] = v[k] = 0.f;
+        ydir[k] = yacc[k] = 0.f;
         s[k] = tvalid ? P.start[b * D + k] : 0.f;
         g[k] = tvalid ? P.goal[b * D + k] : 0.f;
     }
@@ -532,8 +631,8 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
             float a = 0.f, c = 0.f;
 #pragma unroll
             for (int d = 0; d < D; ++d) {
-                a += dP[n * 16 + t * D + d] * P.J[d * D + k];
-                c += dP[(N + n) * 16 + t * D + d] * P.J[d * D + k];
+                a += dP[n * kLd + t * D + d] * P.J[d * D + k];
+                c += dP[(N + n) * kLd + t * D + d] * P.J[d * D + k];
             }
             q[k] = a;
             v[k] = c;
@@ -543,125 +642,129 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
             for (int k = 0; k < D; ++k) P.series[(b * P.max_series) * N * D + n * D + k] = q[k];
         }
     }
-    for (int e = tid; e < NK * 16; e += P.BT) X[e] = 0.f;
-    const float* obs = obsL + (P.obs_stride ? t * P.O * 2 : 0);
+    for (int e = tid; e < MP * kLd; e += P.BT) X[e] = 0.f;
+    const float* obs = obsL + (P.obs_stride ? t * obs_pitch(P.O) : 0);
 
     // replicated per-trajectory scalar state
     float loss = 0.f, lsg = P.lsg0, ljl = P.ljl0, lr = 0.f, cprod = 1.f, gnorm = 1.f, anorm = 0.f;
     float cfac = 1.f, step = 0.f;
-    float s_ds = 0.f, s_dg = 0.f, s_vs = 0.f, s_vg = 0.f, s_tmax = 0.f, s_tmin = 0.f, s_vabs = 0.f;
-    int phase = tvalid ? PH_OUTER_START : PH_DONE, outer = 0, inner = 0, trial = 0, needs_dir = 0;
+    // squared start/goal distances + extrema of the accepted state (constraint check)
+    float s_a0 = 0.f, s_a1 = 0.f, s_b0 = 0.f, s_b1 = 0.f, s_tmax = 0.f, s_tmin = 0.f, s_vabs = 0.f;
+    int phase = tvalid ? PH_OUTER_START : PH_DONE, outer = 0, inner = 0, trial = 0;
+    bool needs_dir = false;
     irm_stats st{};
     st.series_len = rec ? 1 : 0;
+    const unsigned tmask = (1u << D) - 1u;
+    const unsigned fullmask = (ntb >= 32) ? 0xFFFFFFFFu : ((1u << ntb) - 1u);
     __syncthreads();
     IRM_STAMP(14);
 
-    const unsigned tmask = (1u << D) - 1u;
-    for (;;) {
+    for (int round = 0;; ++round) {
         // ------------------------------------------------ direction (stage 1+2)
-        unsigned dirmask = 0;
-        for (int tt = 0; tt < ntb; ++tt)
-            if (flags[tt]) dirmask |= tmask << (tt * D);
+        const unsigned dirmask = flagw[round & 1];
         IRM_STAMP(4);
         if (dirmask) {
-            // active sparse rows of b (start/goal velocity rows, masked velocity-limit rows)
-            if (wave == nwaves - 1) {
-                const int lane = tid & 63;
-                int cnt = 0;
-                for (int base = 0; base < N; base += 64) {
-                    const int nn = base + lane;
-                    const bool f = (nn < N) && act[nn];
-                    const unsigned long long m = __ballot(f);
-                    if (f) list[cnt + __popcll(m & ((1ull << lane) - 1ull))] = nn;
-                    cnt += __popcll(m);
-                }
-                if (lane == 0) list[N] = cnt;
-            }
             // stage 1: Ypart[s] = F_topᵀ(RP × NK) · a   (split-K over the waves)
-            for (int u = wave; u < MT1 * P.nsplit; u += nwaves) {
-                const int tile = u % MT1, sp = u / MT1;
-                const int kq0 = (KQ1 * sp) / P.nsplit, kq1 = (KQ1 * (sp + 1)) / P.nsplit;
-                f32x4 acc = mma_tile(F1, KQ1, tile, kq0, kq1, X);
-                store_tile(Ypart + sp * RP * 16, tile, acc, 0xFFFFu, RP);
+            if (REGOPS) {
+                if (has1) {
+                    const float* xl = X + (lane >> 4) * kLd + (lane & 15);
+                    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int i = 0; i < S1Q; ++i) {
+                        if (kq0 + i < kq1) {
+                            const float* xb = xl + (kq0 + i) * 16 * kLd;
+                            const float b0 = xb[0], b1 = xb[4 * kLd], b2 = xb[8 * kLd], b3 = xb[12 * kLd];
+                            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][0], b0, acc0, 0, 0, 0);
+                            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][1], b1, acc1, 0, 0, 0);
+                            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][2], b2, acc0, 0, 0, 0);
+                            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][3], b3, acc1, 0, 0, 0);
+                        }
+                    }
+                    store_tile(Ypart + sp1 * RP * kLd, tile1, acc0 + acc1, 0xFFFFu, RP);
+                }
+            } else {
+                for (int u = wave; u < MT1 * nsplit; u += nwaves) {
+                    const int tile = u % MT1, sp = u / MT1;
+                    const int k0 = (KQ1 * sp) / nsplit, k1 = (KQ1 * (sp + 1)) / nsplit;
+                    f32x4 acc = mma_tile(F1, KQ1, tile, k0, k1, X);
+                    store_tile(Ypart + sp * RP * kLd, tile, acc, 0xFFFFu, RP);
+                }
             }
+            if (tid == 0) flagw[(round + 1) & 1] = 0u;  // next round's direction mask
             IRM_STAMP(5);
             __syncthreads();
             IRM_STAMP(0);
-            {  // y = Σ partials + Σ_{active rows} F_bot[n]·b[n]
-                const int cnt = list[N];
-                for (int e = tid; e < RP * 16; e += P.BT) {
-                    const int r = e >> 4, c = e & 15;
-                    float y = 0.f;
-                    for (int sp = 0; sp < P.nsplit; ++sp) y += Ypart[sp * RP * 16 + e];
-                    for (int j = 0; j < cnt; ++j) {
-                        const int nn = list[j];
-                        y += Fb[nn * RP + r] * Bs[nn * 16 + c];
-                    }
-                    if ((dirmask >> c) & 1u) Ydir[e] = y;
-                }
-            }
-            __syncthreads();
-            IRM_STAMP(1);
-            // Ymix = Ydir · JᵀJ  (per trajectory D×D)
-            for (int e = tid; e < RP * 16; e += P.BT) {
-                const int r = e >> 4, c = e & 15, tt = c / D, k = c - tt * D;
-                float y = 0.f;
-                if (tt < ntb) {
-#pragma unroll
-                    for (int d = 0; d < D; ++d) y += Ydir[r * 16 + tt * D + d] * P.JtJ[d * D + k];
-                }
-                Ymix[e] = y;
-            }
-            // BLS: partials of W = yᵀy (‖G‖_F and alpha_norm, optimizer_BLS.py:165-166)
-            if (bls && tvalid && needs_dir) {
+            // y = Σ partials; y·JᵀJ; BLS norms.  Lane n = row r of y.
+            float g2 = 0.f, al = 0.f;
+            if (yrow && needs_dir) {
                 float y[D];
 #pragma unroll
-                for (int d = 0; d < D; ++d) y[d] = (n < RP) ? Ydir[n * 16 + t * D + d] : 0.f;
+                for (int d = 0; d < D; ++d) y[d] = 0.f;
+                for (int sp = 0; sp < nsplit; ++sp) {
 #pragma unroll
-                for (int a = 0; a < D; ++a)
+                    for (int d = 0; d < D; ++d) y[d] += Ypart[(sp * RP + n) * kLd + t * D + d];
+                }
 #pragma unroll
-                    for (int c = a; c < D; ++c) {
-                        const float w = wred_sum(y[a] * y[c]);
-                        if ((tid & 63) == 0) wp[wave * D * D + a * D + c] = w;
-                    }
+                for (int k = 0; k < D; ++k) {
+                    float m = 0.f;
+#pragma unroll
+                    for (int d = 0; d < D; ++d) m += y[d] * P.JtJ[d * D + k];
+                    Ymix[n * kLd + t * D + k] = m;
+                    g2 += y[k] * m;        // yᵀ(JᵀJ)y  → ‖G‖²_F
+                    al += P.Jcol[k] * y[k];
+                    ydir[k] = y[k];
+                }
+                al = al * al;              // (uᵀy)²    → Σ_ij (GᵀG)_ij
+            }
+            if (bls && needs_dir) {  // optimizer_BLS.py:165-166 from W = Σ_r y_r y_rᵀ
+                g2 = wred_sum(g2);
+                al = wred_sum(al);
+                if (lane == 0) {
+                    wp[wave * 2] = g2;
+                    wp[wave * 2 + 1] = al;
+                }
             }
             __syncthreads();
             IRM_STAMP(2);
             // stage 2: dP = F(MP × RP) · Ymix, only the direction columns
-            mma_rows(F2, MT2, KQ2, Ymix, dP, dirmask, MP, wave, nwaves);
+            if (REGOPS) {
+                const float* xl = Ymix + (lane >> 4) * kLd + (lane & 15);
+                f32x4 acc[S2T];
+#pragma unroll
+                for (int j = 0; j < S2T; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    if (i < KQ2) {
+                        const float* xb = xl + i * 16 * kLd;
+                        const float b0 = xb[0], b1 = xb[4 * kLd], b2 = xb[8 * kLd], b3 = xb[12 * kLd];
+#pragma unroll
+                        for (int j = 0; j < S2T; ++j) {
+                            if (wave + j * nwaves < MT2) {
+                                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][0], b0, acc[j], 0, 0, 0);
+                                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][1], b1, acc[j], 0, 0, 0);
+                                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][2], b2, acc[j], 0, 0, 0);
+                                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][3], b3, acc[j], 0, 0, 0);
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < S2T; ++j)
+                    if (wave + j * nwaves < MT2) store_tile(dP, wave + j * nwaves, acc[j], dirmask, MP);
+            } else {
+                mma_rows(F2, MT2, KQ2, Ymix, dP, dirmask, MP, wave, nwaves);
+            }
             __syncthreads();
             IRM_STAMP(3);
             if (needs_dir) {
                 if (bls) {
-                    float W[D][D];
-#pragma unroll
-                    for (int a = 0; a < D; ++a)
-#pragma unroll
-                        for (int c = a; c < D; ++c) {
-                            float w = 0.f;
-                            for (int ww = 0; ww < WPT; ++ww) w += wp[(t * WPT + ww) * D * D + a * D + c];
-                            W[a][c] = w;
-                            W[c][a] = w;
-                        }
-                    // GᵀG = J W Jᵀ; ‖G‖² = tr; alpha_norm = Σ_ij (GᵀG)_ij / ‖G‖
-                    float tr = 0.f, all = 0.f;
-#pragma unroll
-                    for (int i = 0; i < D; ++i)
-#pragma unroll
-                        for (int j = 0; j < D; ++j) {
-                            float sacc = 0.f;
-#pragma unroll
-                            for (int a = 0; a < D; ++a) {
-                                float u = 0.f;
-#pragma unroll
-                                for (int c = 0; c < D; ++c) u += W[a][c] * P.J[j * D + c];
-                                sacc += P.J[i * D + a] * u;
-                            }
-                            if (i == j) tr += sacc;
-                            all += sacc;
-                        }
-                    gnorm = sqrtf(tr);
-                    anorm = all / gnorm;
+                    float tg = 0.f, ta = 0.f;
+                    for (int ww = 0; ww < WPT; ++ww) {
+                        tg += wp[(t * WPT + ww) * 2];
+                        ta += wp[(t * WPT + ww) * 2 + 1];
+                    }
+                    gnorm = sqrtf(tg);
+                    anorm = ta / gnorm;
                     st.grad_evals++;  // inner-loop head: cost + grad at α (optimizer_BLS.py:163-164)
                     st.cost_evals++;
                     phase = PH_BLS_TRIAL;
@@ -670,21 +773,22 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                     cfac = 1.f - P.lreg * lr;
                     step = lr;
                 }
-                needs_dir = 0;
+                needs_dir = false;
             }
+        } else if (tid == 0) {
+            flagw[(round + 1) & 1] = 0u;
         }
         if (phase == PH_BLS_TRIAL) {
             cfac = 1.f - P.lreg * lr;
             step = lr / gnorm;
         }
         // ------------------------------------------------------- update
-        for (int e = tid; e < N; e += P.BT) act[e] = 0;
         float q2[D], v2[D];
         if (valid && (phase == PH_GD_INNER || phase == PH_BLS_TRIAL)) {
 #pragma unroll
             for (int k = 0; k < D; ++k) {
-                q2[k] = cfac * q[k] - step * dP[n * 16 + t * D + k];
-                v2[k] = cfac * v[k] - step * dP[(N + n) * 16 + t * D + k];
+                q2[k] = cfac * q[k] - step * dP[n * kLd + t * D + k];
+                v2[k] = cfac * v[k] - step * dP[(N + n) * kLd + t * D + k];
             }
         } else {
 #pragma unroll
@@ -700,26 +804,62 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
         if (ev) {
             if (valid) eval_waypoint<D>(P, q2, v2, obs, w);
             IRM_STAMP(8);
-            eval_partials<D>(P, valid, w, n, wave, q2, v2, s, g, red, sg, t);
+            EvalRed r;
+            r.cmax = valid ? w.cv : -INFINITY;
+            r.cidx = valid ? n : 0x7fffffff;
+            r.usum = valid ? P.one_m_lmax * (w.cv * P.invN) + ljl * ((w.jp + w.jv) * P.invN) : 0.f;
+            r.tx = valid ? w.tx : -INFINITY;
+            r.tn = valid ? w.tn : INFINITY;
+            r.va = valid ? w.va : 0.f;
+            ered_store(r, red, wave);
+            if (valid && (n == 0 || n == N - 1)) {  // trajectory.py:183-204 rows 0 and N−1
+                float a = 0.f, bb = 0.f;
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    const float e = q2[d] - (n == 0 ? s[d] : g[d]);
+                    a += e * e;
+                    bb += v2[d] * v2[d];
+                }
+                sg[t * 4 + (n == 0 ? 0 : 2)] = a;
+                sg[t * 4 + (n == 0 ? 1 : 3)] = bb;
+            }
         }
         IRM_STAMP(9);
         __syncthreads();
         IRM_STAMP(7);
         if (ev) {
+            // combine the trajectory's wave partials (fixed order)
+            const float* r0 = red + (t * WPT) * 10;
+            float cmax = r0[0];
+            int cidx = __float_as_int(r0[1]);
+            float usum = r0[2], tx = r0[3], tn = r0[4], va = r0[5];
+            for (int ww = 1; ww < WPT; ++ww) {
+                const float* rw = red + (t * WPT + ww) * 10;
+                amax_step(cmax, cidx, rw[0], __float_as_int(rw[1]));
+                usum += rw[2];
+                tx = fmaxf(tx, rw[3]);
+                tn = fminf(tn, rw[4]);
+                va = fmaxf(va, rw[5]);
+            }
+            const float e_a0 = sg[t * 4 + 0], e_b0 = sg[t * 4 + 1], e_a1 = sg[t * 4 + 2], e_b1 = sg[t * 4 + 3];
+            const float sgpc = 0.5f * e_a0 + 0.5f * e_a1;                       // trajectory.py:187
+            const float sgvc = 0.5f * e_b0 + 0.5f * e_b1;                       // trajectory.py:203
+            // trajectory.py:85-87 + 281 (mean and joint-limit terms pre-summed in usum)
+            const float nl = (P.lam_max * cmax + usum) + lsg * (sgpc + sgvc);
             const float lsg_e = lsg, ljl_e = ljl;
-            const EvalOut E = eval_finalize(P, red, sg, t, t * WPT, WPT, lsg_e, ljl_e);
             // --------------------------------------------------- decide
             int accept = 0;
             bool snap = false, to_end = false;
-            const float nl = E.loss;
             if (phase == PH_OUTER_START) {  // optimizer_GD.py:422-424 / optimizer_BLS.py:193
                 loss = nl;
                 if (!bls) st.cost_evals++;
                 accept = 2;
                 lr = bls ? P.bls_lr0 : P.gd_lr[outer];
-                needs_dir = 1;
+                needs_dir = true;
                 if (!bls) phase = PH_GD_INNER;
                 if (P.max_inner <= 0) to_end = true;
+            } else if (phase == PH_BLS_REEVAL) {  // gradient at the unchanged α after a fully rejected search
+                needs_dir = true;
             } else if (phase == PH_GD_INNER) {  // optimizer_GD.py:394-408
                 st.grad_evals++;
                 st.cost_evals++;
@@ -732,18 +872,18 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                     st.inner_iterations++;
                     snap = true;
                     if (inner >= P.max_inner) to_end = true;
-                    else needs_dir = 1;
+                    else needs_dir = true;
                 }
             } else {  // PH_BLS_TRIAL: optimizer_BLS.py:136-150, 172-178
                 st.cost_evals++;
                 st.bls_trials++;
                 const float required = loss - P.bls_a * lr * anorm;
-                bool inner_end = false;
+                bool inner_end = false, rejected_all = false;
                 float improve = 0.f;
                 if (nl > required) {
                     lr = lr * P.bls_bm;
                     trial++;
-                    if (trial >= P.max_bls) inner_end = true;  // all rejected: new_loss = loss
+                    if (trial >= P.max_bls) inner_end = rejected_all = true;  // new_loss = loss
                 } else {
                     accept = 1;
                     lr = lr * P.bls_bp;
@@ -759,26 +899,27 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                         st.inner_iterations++;
                         snap = true;
                         if (inner >= P.max_inner) to_end = true;
-                        else needs_dir = 1;
+                        else if (rejected_all) phase = PH_BLS_REEVAL;
+                        else needs_dir = true;
                     }
                 }
             }
             if (accept) {
-                s_ds = E.ds;
-                s_dg = E.dg;
-                s_vs = E.vs;
-                s_vg = E.vg;
-                s_tmax = E.tmax;
-                s_tmin = E.tmin;
-                s_vabs = E.vabs;
+                s_a0 = e_a0;
+                s_a1 = e_a1;
+                s_b0 = e_b0;
+                s_b1 = e_b1;
+                s_tmax = tx;
+                s_tmin = tn;
+                s_vabs = va;
             }
             if (to_end) {  // constraintsFulfilled (trajectory.py:129-137, robot.py:90-113)
-                const bool ok = s_ds < P.eps_p && s_dg < P.eps_p && s_vs < P.eps_v && s_vg < P.eps_v &&
-                                s_tmax <= P.pmax && s_tmin >= P.pmin && s_vabs <= P.vmax;
+                const bool ok = sqrtf(s_a0) < P.eps_p && sqrtf(s_a1) < P.eps_p && sqrtf(s_b0) < P.eps_v &&
+                                sqrtf(s_b1) < P.eps_v && s_tmax <= P.pmax && s_tmin >= P.pmin && s_vabs <= P.vmax;
                 st.outer_iterations++;
                 st.constraints_ok = ok ? 1 : 0;
                 st.final_loss = loss;
-                needs_dir = 0;
+                needs_dir = false;
                 if (ok) {
                     phase = PH_DONE;
                 } else {
@@ -793,15 +934,12 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
             // --------------------------------------------------- gradient inputs at T2
             if (valid) {
                 float a[D], bb[D];
-                grad_waypoint<D>(P, w, q2, v2, n, E.idx, lsg_e, ljl_e, s, g, a, bb);
-                bool any_b = false;
+                grad_waypoint<D>(P, w, q2, v2, n, cidx, lsg_e, ljl_e, s, g, a, bb);
 #pragma unroll
                 for (int k = 0; k < D; ++k) {
-                    X[n * 16 + t * D + k] = a[k];
-                    Bs[n * 16 + t * D + k] = bb[k];
-                    any_b |= (bb[k] != 0.f);
+                    X[n * kLd + t * D + k] = a[k];
+                    Bs[n * kLd + t * D + k] = bb[k];
                 }
-                if (any_b) act[n] = 1;
             }
             IRM_STAMP(12);
             // --------------------------------------------------- accept
@@ -810,12 +948,9 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                 for (int k = 0; k < D; ++k) {
                     q[k] = q2[k];
                     v[k] = v2[k];
+                    yacc[k] = cfac * yacc[k] + step * ydir[k];  // α recovery (rows r = n < RP)
                 }
                 cprod *= cfac;
-                for (int j = n; j < RP * D; j += NW) {  // y_acc ← c·y_acc + s·y  (α recovery)
-                    const int r = j / D, k = j - r * D;
-                    Yacc[r * 16 + t * D + k] = cfac * Yacc[r * 16 + t * D + k] + step * Ydir[r * 16 + t * D + k];
-                }
             }
             // extended-vis snapshot after every non-breaking inner iteration
             // (optimizer_GD.py:366-367, optimizer_BLS.py:106-107)
@@ -828,21 +963,24 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                 st.series_len++;
             }
             if (n == 0) {
-                flags[t] = needs_dir;
-                flags[TB + t] = (phase == PH_DONE);
+                if (needs_dir) atomicOr(&flagw[(round + 1) & 1], tmask << (t * D));
+                if (phase == PH_DONE) atomicOr(&flagw[2], 1u << t);
             }
         }
         IRM_STAMP(15);
         __syncthreads();
         IRM_STAMP(11);
-        int alldone = 1;
-        for (int tt = 0; tt < ntb; ++tt) alldone &= flags[TB + tt];
-        if (alldone) break;
+        if (flagw[2] == fullmask) break;
     }
 
     // ----------------------------------------------------------- epilogue
     // α = cprod·α0 − (V_R·y_acc)·Jᵀ ; trajectory = T ; stats
-    mma_rows(P.Vfrag, NK / 16, RP / 16, Yacc, dP, 0xFFFFu, NK, wave, nwaves);
+    if (yrow) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) Ymix[n * kLd + t * D + k] = yacc[k];
+    }
+    __syncthreads();
+    mma_rows(P.Vfrag, NK / 16, RP / 16, Ymix, dP, 0xFFFFu, NK, wave, nwaves);
     __syncthreads();
     if (valid) {
 #pragma unroll
@@ -851,7 +989,7 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
             if (P.alpha_out) {
                 float acc = 0.f;
 #pragma unroll
-                for (int l = 0; l < D; ++l) acc += dP[n * 16 + t * D + l] * P.J[k * D + l];
+                for (int l = 0; l < D; ++l) acc += dP[n * kLd + t * D + l] * P.J[k * D + l];
                 P.alpha_out[(b * N + n) * D + k] = cprod * alpha0_at<D>(P, b, n, k) - acc;
             }
         }
@@ -887,7 +1025,7 @@ __global__ __launch_bounds__(MAXT) void k_forward(KParams P, int mode) {
     float* sg = smem + L.sg;
     float* obsL = smem + L.obs;
 
-    for (int e = tid; e < P.O * 2; e += P.BT) obsL[e] = P.obstacles[e];
+    stage_obstacles(P, tb0, ntb, obsL);
     stage_alpha<D>(P, tb0, ntb, XG, MP);
     __syncthreads();
     mma_rows(P.Lfrag, MP / 16, NK / 16, XG, Pb, 0xFFFFu, MP, wave, nwaves);
@@ -899,8 +1037,8 @@ __global__ __launch_bounds__(MAXT) void k_forward(KParams P, int mode) {
         if (valid) {
 #pragma unroll
             for (int d = 0; d < D; ++d) {
-                a += Pb[n * 16 + t * D + d] * P.J[d * D + k];
-                c += Pb[(N + n) * 16 + t * D + d] * P.J[d * D + k];
+                a += Pb[n * kLd + t * D + d] * P.J[d * D + k];
+                c += Pb[(N + n) * kLd + t * D + d] * P.J[d * D + k];
             }
         }
         q[k] = a;
@@ -915,7 +1053,7 @@ __global__ __launch_bounds__(MAXT) void k_forward(KParams P, int mode) {
         }
         return;
     }
-    for (int e = tid; e < MP * 16; e += P.BT) XG[e] = 0.f;
+    for (int e = tid; e < MP * kLd; e += P.BT) XG[e] = 0.f;
     WP<D> w;
     if (tvalid) {
         if (valid) eval_waypoint<D>(P, q, v, obsL, w);
@@ -947,8 +1085,8 @@ __global__ __launch_bounds__(MAXT) void k_forward(KParams P, int mode) {
         grad_waypoint<D>(P, w, q, v, n, E.idx, P.lam_sg, P.lam_jl, s, g, a, bb);
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-            XG[n * 16 + t * D + k] = a[k];
-            XG[(N + n) * 16 + t * D + k] = bb[k];
+            XG[n * kLd + t * D + k] = a[k];
+            XG[(N + n) * kLd + t * D + k] = bb[k];
         }
     }
     __syncthreads();
@@ -960,7 +1098,7 @@ __global__ __launch_bounds__(MAXT) void k_forward(KParams P, int mode) {
         for (int k = 0; k < D; ++k) {
             float acc = 0.f;
 #pragma unroll
-            for (int l = 0; l < D; ++l) acc += Pb[n * 16 + t * D + l] * P.J[k * D + l];
+            for (int l = 0; l < D; ++l) acc += Pb[n * kLd + t * D + l] * P.J[k * D + l];
             P.out1[(b * N + n) * D + k] = acc;
         }
     }
@@ -980,7 +1118,7 @@ __global__ void k_fk(KParams P, const float* traj, float* pos, float* jac) {
     for (int d = 0; d < D; ++d) {
         cum += q[d];
         float sn, cs;
-        sincosf(cum, &sn, &cs);
+        sincos_fast(cum, sn, cs);
         fx += P.link[d] * cs;
         fy += P.link[d] * sn;
         xs[d] = -(P.link[d] * sn);
@@ -1082,8 +1220,11 @@ hipError_t launch_optimize(const KParams& p, hipStream_t s) {
         constexpr int DD = decltype(dc)::value;
         return dispatch_t(p.BT, [&](auto tc) {
             constexpr int TT = decltype(tc)::value;
-            return stage ? launch_lds(k_optimize<DD, TT, true>, grid, p.BT, lds, s, p)
-                         : launch_lds(k_optimize<DD, TT, false>, grid, p.BT, lds, s, p);
+            if constexpr (TT <= 512) {
+                if (p.regops) return launch_lds(k_optimize<DD, TT, true, true>, grid, p.BT, lds, s, p);
+            }
+            return stage ? launch_lds(k_optimize<DD, TT, true, false>, grid, p.BT, lds, s, p)
+                         : launch_lds(k_optimize<DD, TT, false, false>, grid, p.BT, lds, s, p);
         });
     });
 }

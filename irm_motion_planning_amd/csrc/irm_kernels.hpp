@@ -10,10 +10,12 @@
 namespace irm {
 
 constexpr int kCols = 16;         // MFMA 16x16x4 column tile = TB·D columns
+constexpr int kLd = 17;           // LDS row stride of [row][16] buffers: odd, so a lane-per-row
+                                  // access (lane n → row n) hits 32 different banks
 constexpr int kMaxThreads = 1024; // one lane per (trajectory, waypoint): TB·NW ≤ 1024
 
 // Per-trajectory phases of the on-device optimiser state machine.
-enum Phase : int32_t { PH_OUTER_START = 0, PH_GD_INNER = 1, PH_BLS_TRIAL = 2, PH_DONE = 3 };
+enum Phase : int32_t { PH_OUTER_START = 0, PH_GD_INNER = 1, PH_BLS_TRIAL = 2, PH_DONE = 3, PH_BLS_REEVAL = 4 };
 
 // Everything a kernel needs, passed by value (kernarg segment).
 struct KParams {
@@ -26,6 +28,7 @@ struct KParams {
     int32_t NW;          // lanes per trajectory = N rounded up to 64 (whole waves)
     int32_t BT;          // threads per workgroup = TB·NW
     int32_t nsplit;      // stage-1 split-K factor
+    int32_t regops;      // operator A-fragments held in VGPRs (k_optimize<…, REGOPS>)
     // optimiser
     int32_t optimizer, max_inner, max_outer, max_bls, cvdl, record_series, max_series, pad0;
     float llr, lci, lsg0, ljl0, eps_p, eps_v, lmax, lreg;
@@ -39,10 +42,11 @@ struct KParams {
     float J[IRM_MAX_JOINTS * IRM_MAX_JOINTS];    // J (D×D, row-major, stride D)
     float JtJ[IRM_MAX_JOINTS * IRM_MAX_JOINTS];  // JᵀJ
     float Jinv[IRM_MAX_JOINTS * IRM_MAX_JOINTS]; // J⁻¹
+    float Jcol[IRM_MAX_JOINTS];                  // u = Jᵀ·1 (column sums): alpha_norm = (uᵀy)²-sum
     // operators (device, fp32)
     const float* Lfrag;   // A-fragments of L = [K;dK]   (MP × NK)
     const float* LTfrag;  // A-fragments of Lᵀ           (NK × MP)
-    const float* F1frag;  // A-fragments of F_topᵀ        (RP × NK)
+    const float* F1frag;  // A-fragments of Fᵀ            (RP × MP)
     const float* F2frag;  // A-fragments of F             (MP × RP)
     const float* Fbot;    // F rows N..2N-1, row-major    (N × RP)
     const float* Vr;      // V_R, row-major               (N × RP)
@@ -87,6 +91,7 @@ __host__ __device__ inline int64_t frag_index(int row, int k, int K) {
 // LDS layout of the optimiser / eval workgroups (float offsets, 16-B aligned).
 struct Plan {
     int f1, f2, fb;              // staged operators F_topᵀ, F, F_bot (optimiser, ops_in_lds)
+    int alist, acnt;             // per-wave lists of active sparse rows (optimiser)
     int X, Bs;                   // MFMA B operand: a (NK × 16) and b (N × 16) / [a; b] (MP × 16)
     int dP;                      // MFMA output rows (MP × 16)
     int Ypart, Ydir, Ymix, Yacc; // stage-1 partials, y, y·JᵀJ, Σ steps·y
@@ -97,6 +102,17 @@ struct Plan {
 };
 
 __host__ __device__ Plan plan_lds(const KParams& p, bool ops_lds, bool optimizer);
+
+// Can the operator A-fragments live in VGPRs (k_optimize<…, REGOPS=true>)?
+// Mirrors kS1Q / kS2T in irm_kernels.hip.
+inline bool regops_fit(const KParams& p) {
+    const int nw = p.BT / 64, MT1 = p.RP / 16, KQ1 = p.MP / 16, KQ2 = p.RP / 16, MT2 = p.MP / 16;
+    if (p.BT > 512 || KQ2 > 2 || MT1 * p.nsplit > nw) return false;
+    const int s1q = p.BT <= 256 ? 8 : 4, s2t = p.BT <= 256 ? 8 : 4;
+    const int kq_per_unit = (KQ1 + p.nsplit - 1) / p.nsplit;
+    const int tiles_per_wave = (MT2 + nw - 1) / nw;
+    return kq_per_unit <= s1q && tiles_per_wave <= s2t;
+}
 
 // launchers (return hipError_t)
 hipError_t launch_init_alpha(const KParams& p, float* alpha_out, hipStream_t s);
