@@ -76,6 +76,11 @@ def make_args(cfg, faithful, max_inner):
         argv += ["--link-length"] + [str(3.0 / D)] * D
     if not faithful:
         argv += ["--loop-loss-reduction=-1e30", "--max-outer-iteration=1", f"--max-inner-iteration={max_inner}"]
+        if D == 7:
+            # The default first step size 2e-3 makes the 7-DoF GD diverge in exact arithmetic
+            # (loss 3e28 after 200 steps; the faithful loop stops at the first increase).  Bench
+            # mode forces every step to run, so C5 uses 1e-3 (converges, same work per step).
+            argv += ["--gd-lr", "1e-3"]
     return irm_main.parse_args(argv)
 
 
@@ -115,6 +120,26 @@ def cpu_baseline(cfg, args, start, goal, obstacles, budget_s=12.0):
                       f"{dt:.2f} s wall on {cores} threads); 1-thread rate {st1[0]['grad_evals'] / t1:.1f} it/s"}
 
 
+def share_environment(obs_t, world):
+    """Rank 0's obstacles to every rank (RCCL broadcast over xGMI; gloo in the CPU tests)."""
+    if world > 1:
+        import torch.distributed as dist
+        dist.broadcast(obs_t, src=0)
+    return obs_t
+
+
+def aggregate(elapsed, iters_rank, world, device):
+    """(max elapsed over ranks, Σ executed iterations over ranks) — the weak-scaling reduction."""
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    it = torch.tensor([iters_rank], dtype=torch.float64, device=device)
+    if world > 1:
+        import torch.distributed as dist
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(it, op=dist.ReduceOp.SUM)
+    return float(t.item()), float(it.item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -148,9 +173,7 @@ def main():
     start, goal, obstacles = make_problem(a.config, world, rank)
 
     # shared environment: rank 0's obstacles broadcast over RCCL/xGMI
-    obs_t = torch.from_numpy(obstacles).to(dev)
-    if world > 1:
-        dist.broadcast(obs_t, src=0)
+    obs_t = share_environment(torch.from_numpy(obstacles).to(dev), world)
     start_t = torch.from_numpy(start).to(dev)
     goal_t = torch.from_numpy(goal).to(dev)
     alpha_t = torch.empty((B, N, D), dtype=torch.float32, device=dev)
@@ -186,13 +209,7 @@ def main():
 
     st = stats_t.cpu().numpy()
     iters_rank = float(st[:, 2].sum())  # grad_evals = executed inner iterations
-    t_tensor = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    it_tensor = torch.tensor([iters_rank], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t_tensor, op=dist.ReduceOp.MAX)
-        dist.all_reduce(it_tensor, op=dist.ReduceOp.SUM)
-    elapsed_max = float(t_tensor.item())
-    iters_all = float(it_tensor.item())
+    elapsed_max, iters_all = aggregate(elapsed, iters_rank, world, dev)
     value = iters_all * a.steps / elapsed_max
 
     exec_f, ref_f = flops_per_iteration(N, D, O, info["operator_rank"])
@@ -216,7 +233,8 @@ def main():
             "workload": f"{a.config}: {desc}",
             "batch_per_gpu": B, "global_batch": B * world, "n_timesteps": N, "n_joints": D, "n_obstacles": O,
             "optimizer": opt, "mode": "faithful" if a.faithful else f"bench ({a.max_inner} fixed GD iterations)",
-            "operator_rank": info["operator_rank"], "traj_per_block": info["traj_per_block"],
+            "operator_rank": info["operator_rank"],
+            "traj_per_block": a.tb or min(info["traj_per_block"], -(-B // info["num_cus"])),
             "parallelism": f"dp{world} (batch sharded, env broadcast over RCCL)",
         },
         "roofline": {

@@ -167,8 +167,8 @@ struct irm_ctx {
     std::vector<float> t, cvec, K, dK, J;
     KParams kp{};
     // device
-    float *d_Lfrag = nullptr, *d_LTfrag = nullptr, *d_F1 = nullptr, *d_F2 = nullptr, *d_Fbot = nullptr,
-          *d_Vr = nullptr, *d_Vfrag = nullptr, *d_u = nullptr, *d_w = nullptr;
+    float *d_K = nullptr, *d_dK = nullptr, *d_Kt = nullptr, *d_dKt = nullptr, *d_F1 = nullptr, *d_F2 = nullptr,
+          *d_Fbot = nullptr, *d_Vr = nullptr, *d_Vfrag = nullptr, *d_u = nullptr, *d_w = nullptr;
     // host-API staging
     void* d_io = nullptr;
     size_t io_bytes = 0;
@@ -442,16 +442,19 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
     std::vector<double> A;
     std::vector<float> frag;
     int rc = 0;
-    A.assign((size_t)MP * NK, 0.0);  // L (MP × NK)
-    for (int m = 0; m < 2 * N; ++m)
-        for (int j = 0; j < N; ++j) A[(size_t)m * NK + j] = Ld[(size_t)m * N + j];
-    fill_frag(frag, MP, NK, A);
-    rc |= upload(&c->d_Lfrag, frag);
-    A.assign((size_t)NK * MP, 0.0);  // Lᵀ (NK × MP)
-    for (int m = 0; m < 2 * N; ++m)
-        for (int j = 0; j < N; ++j) A[(size_t)j * MP + m] = Ld[(size_t)m * N + j];
-    fill_frag(frag, NK, MP, A);
-    rc |= upload(&c->d_LTfrag, frag);
+    {  // K, dK and their transposes, row-major fp32: the correctly rounded α-space
+       // contractions (eval_exact / grad_exact) read one coalesced row per k-step
+        std::vector<float> kt((size_t)N * N), dkt((size_t)N * N);
+        for (int i = 0; i < N; ++i)
+            for (int j = 0; j < N; ++j) {
+                kt[(size_t)j * N + i] = c->K[(size_t)i * N + j];
+                dkt[(size_t)j * N + i] = c->dK[(size_t)i * N + j];
+            }
+        rc |= upload(&c->d_K, c->K);
+        rc |= upload(&c->d_dK, c->dK);
+        rc |= upload(&c->d_Kt, kt);
+        rc |= upload(&c->d_dKt, dkt);
+    }
     A.assign((size_t)RP * MP, 0.0);  // Fᵀ (RP × MP): stage 1 contracts y = Fᵀ·[a; b]
     for (int m = 0; m < 2 * N; ++m)
         for (int r = 0; r < RP; ++r) A[(size_t)r * MP + m] = F[(size_t)m * RP + r];
@@ -575,8 +578,10 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
             kp.Jinv[i] = Jinv[i];
         }
     }
-    kp.Lfrag = c->d_Lfrag;
-    kp.LTfrag = c->d_LTfrag;
+    kp.Km = c->d_K;
+    kp.dKm = c->d_dK;
+    kp.Kt = c->d_Kt;
+    kp.dKt = c->d_dKt;
     kp.F1frag = c->d_F1;
     kp.F2frag = c->d_F2;
     kp.Fbot = c->d_Fbot;
@@ -611,7 +616,8 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
 void irm_ctx_destroy(irm_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->p.device);
-    float* bufs[] = {c->d_Lfrag, c->d_LTfrag, c->d_F1, c->d_F2, c->d_Fbot, c->d_Vr, c->d_Vfrag, c->d_u, c->d_w};
+    float* bufs[] = {c->d_K, c->d_dK, c->d_Kt, c->d_dKt, c->d_F1,   c->d_F2,
+                     c->d_Fbot, c->d_Vr, c->d_Vfrag, c->d_u, c->d_w};
     for (float* b : bufs)
         if (b) (void)hipFree(b);
     if (c->d_io) (void)hipFree(c->d_io);

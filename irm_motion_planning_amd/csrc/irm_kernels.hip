@@ -62,7 +62,7 @@ __host__ __device__ Plan plan_lds(const KParams& p, bool ops_lds, bool optimizer
     L.red = take(nw * 10);
     L.sg = take(TB * 4);
     L.wp = take(nw * 2);
-    L.flags = take(4);
+    L.flags = take(8);
     L.act = L.list = 0;
     L.obs = take((p.obs_stride ? TB : 1) * ((p.O + 3) & ~3) * 2 + 4);
     L.total = off;
@@ -463,15 +463,85 @@ __device__ void stage_alpha(const KParams& P, int tb0, int ntb, float* X, int xr
     }
 }
 
+// ------------------------------------------- correctly rounded α-space maps
+// The reference's K@α@J (trajectory.py:63-65) contracts over N waypoints with
+// |α| ≈ 1e3 (singular K): a plain fp32 sum carries ~1e-4 (positions) and
+// ~1e-3 (velocities) of order-dependent noise.  Here every product of two
+// fp32 values is exact in fp64 and the N-term sum accumulates in fp64 (same
+// sequential order as oracle/irm_oracle.c), then rounds once — the result is
+// the correctly rounded fp32 value, bit-identical to the CPU oracle.  Used off
+// the hot loop: host-API evaluation and the optimiser's prologue / resyncs.
+//
+// Lane n of trajectory column block Xa (LDS, rows m = 0..N-1, stride kLd):
+//   q = fp32(fp32(K·α)[n]·J), v = fp32(fp32(dK·α)[n]·J).
 template <int D>
-__device__ __forceinline__ float alpha0_at(const KParams& P, size_t b, int n, int k) {
-    if (P.alpha0) return P.alpha0[(b * P.N + n) * D + k];
-    float sj = 0.f, gj = 0.f;
-    for (int e2 = 0; e2 < D; ++e2) {
-        sj += P.start[b * D + e2] * P.Jinv[e2 * D + k];
-        gj += P.goal[b * D + e2] * P.Jinv[e2 * D + k];
+__device__ void eval_exact(const KParams& P, const float* __restrict__ Xa, int n, float (&q)[D], float (&v)[D]) {
+    const int N = P.N;
+    double aq[D], av[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) aq[d] = av[d] = 0.0;
+    const float* kt = P.Kt + n;
+    const float* dkt = P.dKt + n;
+    for (int m = 0; m < N; ++m) {
+        const double kq = (double)kt[(size_t)m * N], kv = (double)dkt[(size_t)m * N];  // K[n][m], dK[n][m]
+        const float* xr = Xa + m * kLd;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const double x = (double)xr[d];
+            aq[d] = fma(kq, x, aq[d]);
+            av[d] = fma(kv, x, av[d]);
+        }
     }
-    return P.uvec[n] * sj + P.wvec[n] * gj;
+    float tq[D], tv[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        tq[d] = (float)aq[d];
+        tv[d] = (float)av[d];
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        double sq = 0.0, sv = 0.0;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            sq = fma((double)tq[d], (double)P.J[d * D + k], sq);
+            sv = fma((double)tv[d], (double)P.J[d * D + k], sv);
+        }
+        q[k] = (float)sq;
+        v[k] = (float)sv;
+    }
+}
+
+// G[n] = (fp32(Kᵀa)[n] + fp32(dKᵀb)[n])·Jᵀ  (trajectory.py:295), the N-sums
+// in fp64 as above, the fp32 add and the D-term J product unfused in fp32
+// (the oracle's order).  Xa: a in rows 0..N-1, b in rows N..2N-1.
+template <int D>
+__device__ void grad_exact(const KParams& P, const float* __restrict__ Xa, int n, float (&G)[D]) {
+    const int N = P.N;
+    double ga[D], gb[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) ga[d] = gb[d] = 0.0;
+    const float* km = P.Km + n;
+    const float* dkm = P.dKm + n;
+    for (int m = 0; m < N; ++m) {
+        const double ka = (double)km[(size_t)m * N], kb = (double)dkm[(size_t)m * N];  // K[m][n], dK[m][n]
+        const float* xa = Xa + m * kLd;
+        const float* xb = Xa + (N + m) * kLd;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            ga[d] = fma(ka, (double)xa[d], ga[d]);
+            gb[d] = fma(kb, (double)xb[d], gb[d]);
+        }
+    }
+    float tmp[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) tmp[d] = __fadd_rn((float)ga[d], (float)gb[d]);
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        float u = 0.f;
+#pragma unroll
+        for (int l = 0; l < D; ++l) u = __fadd_rn(u, __fmul_rn(tmp[l], P.J[k * D + l]));
+        G[k] = u;
+    }
 }
 
 // ------------------------------------------------------------ optimiser
@@ -609,47 +679,38 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
     stage_obstacles(P, tb0, ntb, obsL);
     for (int e = tid; e < RP * kLd; e += P.BT) Ymix[e] = 0.f;
     if (tid == 0) {
-        flagw[0] = flagw[1] = 0u;
-        flagw[2] = 0u;
+        flagw[0] = flagw[1] = 0u;  // direction masks (bit per column), by round parity
+        flagw[2] = 0u;             // done mask (bit per trajectory)
+        flagw[3] = flagw[4] = 0u;  // resync masks (bit per trajectory), by round parity
     }
     stage_alpha<D>(P, tb0, ntb, X, NK);
     __syncthreads();
-    // T0 = (K·α0)·J, V0 = (dK·α0)·J  (trajectory.py:63-65)
-    mma_rows(P.Lfrag, MT2, NK / 16, X, dP, 0xFFFFu, MP, wave, nwaves);
-    __syncthreads();
-    float q[D], v[D], s[D], g[D], ydir[D], yacc[D];
+    // T0 = (K·α0)·J, V0 = (dK·α0)·J  (trajectory.py:63-65), correctly rounded.
+    // ab: this lane's row of the α the state is currently expressed against
+    // (α = cprod·ab − (V_R·yacc)·Jᵀ); α0 now, the materialised α after a resync.
+    float q[D], v[D], s[D], g[D], ydir[D], yacc[D], ab[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) {
         q[k] = v[k] = 0.f;
         ydir[k] = yacc[k] = 0.f;
+        ab[k] = valid ? X[n * kLd + t * D + k] : 0.f;
         s[k] = tvalid ? P.start[b * D + k] : 0.f;
         g[k] = tvalid ? P.goal[b * D + k] : 0.f;
     }
     if (valid) {
-#pragma unroll
-        for (int k = 0; k < D; ++k) {
-            float a = 0.f, c = 0.f;
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                a += dP[n * kLd + t * D + d] * P.J[d * D + k];
-                c += dP[(N + n) * kLd + t * D + d] * P.J[d * D + k];
-            }
-            q[k] = a;
-            v[k] = c;
-        }
+        eval_exact<D>(P, X + t * D, n, q, v);
         if (rec) {
 #pragma unroll
             for (int k = 0; k < D; ++k) P.series[(b * P.max_series) * N * D + n * D + k] = q[k];
         }
     }
+    __syncthreads();  // every lane has read α0 from X
     for (int e = tid; e < MP * kLd; e += P.BT) X[e] = 0.f;
     const float* obs = obsL + (P.obs_stride ? t * obs_pitch(P.O) : 0);
 
     // replicated per-trajectory scalar state
     float loss = 0.f, lsg = P.lsg0, ljl = P.ljl0, lr = 0.f, cprod = 1.f, gnorm = 1.f, anorm = 0.f;
     float cfac = 1.f, step = 0.f;
-    // squared start/goal distances + extrema of the accepted state (constraint check)
-    float s_a0 = 0.f, s_a1 = 0.f, s_b0 = 0.f, s_b1 = 0.f, s_tmax = 0.f, s_tmin = 0.f, s_vabs = 0.f;
     int phase = tvalid ? PH_OUTER_START : PH_DONE, outer = 0, inner = 0, trial = 0;
     bool needs_dir = false;
     irm_stats st{};
@@ -782,6 +843,55 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
             cfac = 1.f - P.lreg * lr;
             step = lr / gnorm;
         }
+        // ------------------------------------------------------- resync
+        // Trajectories whose inner loop ended last round: α = cprod·ab −
+        // (V_R·yacc)·Jᵀ in fp32 (what the reference carries), then [T; V] =
+        // eval_exact(α), so the constraint check below and the caller's
+        // evaluate(α_out) see the same waypoints bit for bit.
+        const unsigned rmask = flagw[3 + (round & 1)];
+        if (tid == 0) flagw[3 + ((round + 1) & 1)] = 0u;
+        if (rmask) {  // block-uniform
+            const bool rs = tvalid && ((rmask >> t) & 1u);  // wave-uniform
+            if (rs && yrow) {
+#pragma unroll
+                for (int k = 0; k < D; ++k) Ymix[n * kLd + t * D + k] = yacc[k];
+            }
+            __syncthreads();
+            if (rs && valid) {
+                float z[D];
+#pragma unroll
+                for (int l = 0; l < D; ++l) z[l] = 0.f;
+                const float* vr = P.Vr + (size_t)n * RP;
+                for (int r = 0; r < RP; ++r) {
+                    const float vv = vr[r];
+#pragma unroll
+                    for (int l = 0; l < D; ++l) z[l] += vv * Ymix[r * kLd + t * D + l];
+                }
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int l = 0; l < D; ++l) acc += z[l] * P.J[k * D + l];
+                    ab[k] = cprod * ab[k] - acc;
+                    X[n * kLd + t * D + k] = ab[k];
+                }
+            }
+            __syncthreads();
+            if (rs) {
+                if (valid) {
+                    eval_exact<D>(P, X + t * D, n, q, v);
+                    // the last extended-vis frame shows the materialised α's trajectory
+                    if (rec && st.series_len > 0) {
+#pragma unroll
+                        for (int k = 0; k < D; ++k)
+                            P.series[((b * P.max_series) + st.series_len - 1) * N * D + n * D + k] = q[k];
+                    }
+                }
+                cprod = 1.f;
+#pragma unroll
+                for (int k = 0; k < D; ++k) yacc[k] = 0.f;
+            }
+        }
         // ------------------------------------------------------- update
         float q2[D], v2[D];
         if (valid && (phase == PH_GD_INNER || phase == PH_BLS_TRIAL)) {
@@ -860,6 +970,22 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                 if (P.max_inner <= 0) to_end = true;
             } else if (phase == PH_BLS_REEVAL) {  // gradient at the unchanged α after a fully rejected search
                 needs_dir = true;
+            } else if (phase == PH_RESYNC) {
+                // constraintsFulfilled(α) (trajectory.py:129-137, robot.py:90-113) on the
+                // materialised α; optimizer_GD.py:427-437 / optimizer_BLS.py:201-211
+                const bool ok = sqrtf(e_a0) < P.eps_p && sqrtf(e_a1) < P.eps_p && sqrtf(e_b0) < P.eps_v &&
+                                sqrtf(e_b1) < P.eps_v && tx <= P.pmax && tn >= P.pmin && va <= P.vmax;
+                st.outer_iterations++;
+                st.constraints_ok = ok ? 1 : 0;
+                if (ok) {
+                    phase = PH_DONE;
+                } else {
+                    outer++;
+                    lsg = lsg * P.lci;
+                    ljl = ljl * P.lci;
+                    inner = 0;
+                    phase = (outer >= P.max_outer) ? PH_DONE : PH_OUTER_START;
+                }
             } else if (phase == PH_GD_INNER) {  // optimizer_GD.py:394-408
                 st.grad_evals++;
                 st.cost_evals++;
@@ -904,31 +1030,10 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                     }
                 }
             }
-            if (accept) {
-                s_a0 = e_a0;
-                s_a1 = e_a1;
-                s_b0 = e_b0;
-                s_b1 = e_b1;
-                s_tmax = tx;
-                s_tmin = tn;
-                s_vabs = va;
-            }
-            if (to_end) {  // constraintsFulfilled (trajectory.py:129-137, robot.py:90-113)
-                const bool ok = sqrtf(s_a0) < P.eps_p && sqrtf(s_a1) < P.eps_p && sqrtf(s_b0) < P.eps_v &&
-                                sqrtf(s_b1) < P.eps_v && s_tmax <= P.pmax && s_tmin >= P.pmin && s_vabs <= P.vmax;
-                st.outer_iterations++;
-                st.constraints_ok = ok ? 1 : 0;
+            if (to_end) {  // inner loop over: materialise α next round, then check constraints
                 st.final_loss = loss;
                 needs_dir = false;
-                if (ok) {
-                    phase = PH_DONE;
-                } else {
-                    outer++;
-                    lsg = lsg * P.lci;
-                    ljl = ljl * P.lci;
-                    inner = 0;
-                    phase = (outer >= P.max_outer) ? PH_DONE : PH_OUTER_START;
-                }
+                phase = PH_RESYNC;
             }
             IRM_STAMP(10);
             // --------------------------------------------------- gradient inputs at T2
@@ -965,6 +1070,7 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
             if (n == 0) {
                 if (needs_dir) atomicOr(&flagw[(round + 1) & 1], tmask << (t * D));
                 if (phase == PH_DONE) atomicOr(&flagw[2], 1u << t);
+                if (phase == PH_RESYNC) atomicOr(&flagw[3 + ((round + 1) & 1)], 1u << t);
             }
         }
         IRM_STAMP(15);
@@ -990,7 +1096,7 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                 float acc = 0.f;
 #pragma unroll
                 for (int l = 0; l < D; ++l) acc += dP[n * kLd + t * D + l] * P.J[k * D + l];
-                P.alpha_out[(b * N + n) * D + k] = cprod * alpha0_at<D>(P, b, n, k) - acc;
+                P.alpha_out[(b * N + n) * D + k] = cprod * ab[k] - acc;
             }
         }
     }
@@ -1008,8 +1114,7 @@ __global__ __launch_bounds__(MAXT) void k_forward(KParams P, int mode) {
     const Plan L = plan_lds(P, false, false);
     const int tid = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nwaves = P.BT >> 6;
-    const int N = P.N, NW = P.NW, TB = P.TB, MP = P.MP, NK = P.NK;
+    const int N = P.N, NW = P.NW, TB = P.TB, MP = P.MP;
     const int WPT = NW >> 6;
     const int t = wave / WPT;
     const int n = tid - t * NW;
@@ -1020,7 +1125,6 @@ __global__ __launch_bounds__(MAXT) void k_forward(KParams P, int mode) {
     const bool valid = tvalid && n < N;
     const size_t b = (size_t)(tb0 + (tvalid ? t : 0));
     float* XG = smem + L.X;
-    float* Pb = smem + L.dP;
     float* red = smem + L.red;
     float* sg = smem + L.sg;
     float* obsL = smem + L.obs;
@@ -1028,24 +1132,15 @@ __global__ __launch_bounds__(MAXT) void k_forward(KParams P, int mode) {
     stage_obstacles(P, tb0, ntb, obsL);
     stage_alpha<D>(P, tb0, ntb, XG, MP);
     __syncthreads();
-    mma_rows(P.Lfrag, MP / 16, NK / 16, XG, Pb, 0xFFFFu, MP, wave, nwaves);
-    __syncthreads();
     float q[D], v[D], s[D], g[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) {
-        float a = 0.f, c = 0.f;
-        if (valid) {
-#pragma unroll
-            for (int d = 0; d < D; ++d) {
-                a += Pb[n * kLd + t * D + d] * P.J[d * D + k];
-                c += Pb[(N + n) * kLd + t * D + d] * P.J[d * D + k];
-            }
-        }
-        q[k] = a;
-        v[k] = c;
+        q[k] = v[k] = 0.f;
         s[k] = tvalid ? P.start[b * D + k] : 0.f;
         g[k] = tvalid ? P.goal[b * D + k] : 0.f;
     }
+    if (valid) eval_exact<D>(P, XG + t * D, n, q, v);
+    __syncthreads();
     if (mode == 0) {
         if (valid) {
 #pragma unroll
@@ -1053,7 +1148,6 @@ __global__ __launch_bounds__(MAXT) void k_forward(KParams P, int mode) {
         }
         return;
     }
-    for (int e = tid; e < MP * kLd; e += P.BT) XG[e] = 0.f;
     WP<D> w;
     if (tvalid) {
         if (valid) eval_waypoint<D>(P, q, v, obsL, w);
@@ -1090,17 +1184,12 @@ __global__ __launch_bounds__(MAXT) void k_forward(KParams P, int mode) {
         }
     }
     __syncthreads();
-    // G = (Lᵀ·[a; b])·Jᵀ  (trajectory.py:295)
-    mma_rows(P.LTfrag, NK / 16, MP / 16, XG, Pb, 0xFFFFu, NK, wave, nwaves);
-    __syncthreads();
+    // G = (Kᵀa + dKᵀb)·Jᵀ  (trajectory.py:295)
     if (valid) {
+        float G[D];
+        grad_exact<D>(P, XG + t * D, n, G);
 #pragma unroll
-        for (int k = 0; k < D; ++k) {
-            float acc = 0.f;
-#pragma unroll
-            for (int l = 0; l < D; ++l) acc += Pb[n * kLd + t * D + l] * P.J[k * D + l];
-            P.out1[(b * N + n) * D + k] = acc;
-        }
+        for (int k = 0; k < D; ++k) P.out1[(b * N + n) * D + k] = G[k];
     }
 }
 

@@ -15,7 +15,16 @@ constexpr int kLd = 17;           // LDS row stride of [row][16] buffers: odd, s
 constexpr int kMaxThreads = 1024; // one lane per (trajectory, waypoint): TB·NW ≤ 1024
 
 // Per-trajectory phases of the on-device optimiser state machine.
-enum Phase : int32_t { PH_OUTER_START = 0, PH_GD_INNER = 1, PH_BLS_TRIAL = 2, PH_DONE = 3, PH_BLS_REEVAL = 4 };
+// PH_RESYNC: an inner loop has ended; α is materialised in fp32, [T; V] is
+// re-evaluated from it exactly and constraintsFulfilled(α) decides the outer step.
+enum Phase : int32_t {
+    PH_OUTER_START = 0,
+    PH_GD_INNER = 1,
+    PH_BLS_TRIAL = 2,
+    PH_DONE = 3,
+    PH_BLS_REEVAL = 4,
+    PH_RESYNC = 5
+};
 
 // Everything a kernel needs, passed by value (kernarg segment).
 struct KParams {
@@ -44,8 +53,10 @@ struct KParams {
     float Jinv[IRM_MAX_JOINTS * IRM_MAX_JOINTS]; // J⁻¹
     float Jcol[IRM_MAX_JOINTS];                  // u = Jᵀ·1 (column sums): alpha_norm = (uᵀy)²-sum
     // operators (device, fp32)
-    const float* Lfrag;   // A-fragments of L = [K;dK]   (MP × NK)
-    const float* LTfrag;  // A-fragments of Lᵀ           (NK × MP)
+    const float* Km;      // K, row-major                 (N × N)
+    const float* dKm;     // dK, row-major                (N × N)
+    const float* Kt;      // Kᵀ, row-major                (N × N)
+    const float* dKt;     // dKᵀ, row-major               (N × N)
     const float* F1frag;  // A-fragments of Fᵀ            (RP × MP)
     const float* F2frag;  // A-fragments of F             (MP × RP)
     const float* Fbot;    // F rows N..2N-1, row-major    (N × RP)

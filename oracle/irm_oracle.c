@@ -158,13 +158,20 @@ void orc_default_jac(int32_t D, float jgm, uint32_t seed, float* jac_out) {
 
 /* ------------------------------------------------------------- evaluation */
 
-/* C(m×n) = A(m×k) @ B(k×n), fp32, dot products in k order. */
+/* C(m×n) = A(m×k) @ B(k×n) on fp32 operands; each dot product accumulates in
+   fp64 and is rounded once to fp32.  The reference's contractions are XLA/BLAS
+   blocked fp32 GEMMs whose summation order is unspecified; with the singular K
+   (|α| ≈ 1e3 after initTrajectory, larger after the dual loop escalates λ) a
+   plain sequential fp32 sum drifts by >1e-2 in waypoint space late in the dual
+   loop and sends the chaotic BLS into another basin.
+   The correctly-rounded product is order independent and matches the
+   reference run with fp64 *or* BLAS evaluation (tests/golden c2 case). */
 static void matmul(const float* A, const float* B, float* C, int m, int k, int n) {
     for (int i = 0; i < m; ++i)
         for (int j = 0; j < n; ++j) {
-            float s = 0.f;
-            for (int l = 0; l < k; ++l) s += A[i * k + l] * B[l * n + j];
-            C[i * n + j] = s;
+            double s = 0.0;
+            for (int l = 0; l < k; ++l) s += (double)A[i * k + l] * (double)B[l * n + j];
+            C[i * n + j] = (float)s;
         }
 }
 
@@ -369,10 +376,10 @@ void orc_cost_g(const orc_ctx* c, const float* alpha, const float* obstacles, in
     /* (K^T @ ta + dK^T @ tb) @ J^T */
     for (int n = 0; n < N; ++n)
         for (int k = 0; k < D; ++k) {
-            float u = 0.f, v = 0.f;
-            for (int m = 0; m < N; ++m) u += c->K[m * N + n] * ta[m * D + k];
-            for (int m = 0; m < N; ++m) v += c->dK[m * N + n] * tb[m * D + k];
-            tmp[n * D + k] = u + v;
+            double u = 0.0, v = 0.0; /* fp64 accumulation, rounded once (see matmul) */
+            for (int m = 0; m < N; ++m) u += (double)c->K[m * N + n] * (double)ta[m * D + k];
+            for (int m = 0; m < N; ++m) v += (double)c->dK[m * N + n] * (double)tb[m * D + k];
+            tmp[n * D + k] = (float)u + (float)v;
         }
     for (int n = 0; n < N; ++n)
         for (int k = 0; k < D; ++k) {

@@ -1,0 +1,410 @@
+"""HIP path vs the reference (golden vectors) and vs the CPU oracle, through the C ABI.
+
+Run on an MI355X: `pytest -m gpu`.  Every call below lands in a gfx950 kernel of
+libirm_hip.so; there is no host fallback (a missing library / device raises).
+
+Tolerances, written per test:
+  * well-conditioned α: cost rtol 1e-5, gradient 1e-5·max|G|, waypoints 1e-5;
+  * α0 of the singular initTrajectory solve: waypoints atol 5e-4, velocities 5e-3
+    (fp32 summation-order noise of K@α with |α| ≈ 1e3, present in the reference);
+  * GD iterates: atol 1e-3 for k ≤ 5 steps, 1e-2 after 200 steps;
+  * chaotic BLS / noise-terminated dual loops: final avg/max obstacle cost and the
+    constraint flag inside the reference's own ±1-ulp ensemble (conftest.check_quality).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import E2E_CASES, GOAL, START, check_quality, obstacles, oracle_for, params
+
+pytestmark = pytest.mark.gpu
+
+_CTX = {}
+
+
+def ctx(*argv, **overrides):
+    from irm_motion_planning_amd.context import Context
+    key = (tuple(str(a) for a in argv), tuple(sorted(overrides.items())))
+    if key not in _CTX:
+        _CTX[key] = Context(params(*argv, **overrides))
+    return _CTX[key]
+
+
+# ----------------------------------------------------------------- building blocks
+
+def test_device_is_gfx950():
+    info = ctx().info()
+    assert info["arch"].startswith("gfx950"), info
+    assert info["num_cus"] >= 200 and 0 < info["operator_rank"] <= 32
+
+
+@pytest.mark.parametrize("N", [50, 64, 128, 256])
+def test_kernel_matrices(g_setup, N):
+    t, K, dK, J = ctx("--n-timesteps", N).kernel_matrices()
+    np.testing.assert_array_equal(t, g_setup[f"t_{N}"])
+    np.testing.assert_array_equal(J, g_setup["J"])
+    if N <= 64:
+        np.testing.assert_allclose(K, g_setup[f"K_{N}"], rtol=1e-6, atol=2e-7)
+        np.testing.assert_allclose(dK, g_setup[f"dK_{N}"], rtol=1e-6, atol=2e-6)
+    else:
+        r = [0, N // 2, N - 1]
+        np.testing.assert_allclose(K[r], g_setup[f"Krows_{N}"], rtol=1e-6, atol=2e-7)
+        np.testing.assert_allclose(dK[r], g_setup[f"dKrows_{N}"], rtol=1e-6, atol=2e-6)
+
+
+@pytest.mark.parametrize("name", ["alpha0", "small1", "small2"])
+def test_evaluate(g_eval, name):
+    c = ctx()
+    a = g_eval[name]
+    tol_t, tol_v = (5e-4, 5e-3) if name == "alpha0" else (1e-5, 5e-5)
+    np.testing.assert_allclose(c.evaluate(a, 0), g_eval[name + "_traj"], rtol=0, atol=tol_t)
+    np.testing.assert_allclose(c.evaluate(a, 1), g_eval[name + "_vel"], rtol=0, atol=tol_v)
+
+
+@pytest.mark.parametrize("name", ["small1", "small2"])
+def test_cost_and_grad_exact(g_eval, name):
+    c = ctx()
+    a, obs = g_eval[name], g_eval["obstacles"]
+    for i, lam in enumerate(g_eval["lams"]):
+        cost = c.eval_cost(a, obs, g_eval["start"], g_eval["goal"], *lam)
+        grad, cost2 = c.eval_cost_grad(a, obs, g_eval["start"], g_eval["goal"], *lam, with_cost=True)
+        ref_c, ref_g = g_eval[name + "_cost"][i], g_eval[name + "_grad"][i]
+        assert abs(cost - ref_c) <= 1e-5 * abs(ref_c) + 1e-6, (lam, cost, ref_c)
+        assert abs(cost2 - ref_c) <= 1e-5 * abs(ref_c) + 1e-6, (lam, cost2, ref_c)
+        assert np.abs(grad - ref_g).max() <= 1e-5 * np.abs(ref_g).max(), lam
+
+
+def test_cost_and_grad_at_alpha0(g_eval):
+    """Same bands as the oracle's test: the α0 velocity noise times λ_sg dominates."""
+    c = ctx()
+    a, obs = g_eval["alpha0"], g_eval["obstacles"]
+    for i, lam in enumerate(g_eval["lams"]):
+        cost = c.eval_cost(a, obs, g_eval["start"], g_eval["goal"], *lam)
+        grad = c.eval_cost_grad(a, obs, g_eval["start"], g_eval["goal"], *lam)
+        ref_c, ref_g = g_eval["alpha0_cost"][i], g_eval["alpha0_grad"][i]
+        assert abs(cost - ref_c) <= 2e-4 * abs(ref_c), (lam, cost, ref_c)
+        tol = 1e-3 if lam[0] == 0 else 0.1
+        assert np.abs(grad - ref_g).max() <= tol * np.abs(ref_g).max(), lam
+
+
+def test_batched_cost_grad_matches_oracle():
+    """Batch of 37 random well-conditioned α with per-problem start/goal (B not a multiple of anything)."""
+    c, o = ctx(), oracle_for()
+    rng = np.random.default_rng(7)
+    a = (rng.standard_normal((37, 50, 3)) * 0.2).astype(np.float32)
+    s = rng.uniform(-0.5, 0.5, (37, 3)).astype(np.float32)
+    g = rng.uniform(0.2, 1.6, (37, 3)).astype(np.float32)
+    obs = obstacles()
+    grad, cost = c.eval_cost_grad(a, obs, s, g, 0.5, 0.1, 0.5, with_cost=True)
+    for b in range(0, 37, 6):
+        rc = o.cost(a[b], obs, s[b], g[b], 0.5, 0.1, 0.5)
+        rg = o.cost_g(a[b], obs, s[b], g[b], 0.5, 0.1, 0.5)
+        assert abs(cost[b] - rc) <= 1e-5 * abs(rc)
+        assert np.abs(grad[b] - rg).max() <= 1e-5 * np.abs(rg).max()
+
+
+@pytest.mark.parametrize("name", ["alpha0", "small1", "small2"])
+def test_fk_jacobian_potential(g_eval, name):
+    c = ctx()
+    traj = g_eval[name + "_traj"]
+    pos, jac = c.fk(traj, with_jacobian=True)
+    np.testing.assert_allclose(pos, g_eval[name + "_fk"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(jac, g_eval[name + "_jac"], rtol=0, atol=1e-6)
+    cv, cg = c.compute_cost_vg(g_eval[name + "_fk"], g_eval["obstacles"])
+    np.testing.assert_allclose(cv, g_eval[name + "_cost_v"], rtol=2e-6, atol=0)
+    np.testing.assert_allclose(cg, g_eval[name + "_cost_g"], rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("name", ["alpha0", "small1", "small2"])
+def test_constraints(g_eval, name):
+    c, o = ctx(), oracle_for()
+    ok, rep = c.constraints(g_eval[name], g_eval["start"], g_eval["goal"])
+    assert ok == bool(g_eval[name + "_ok"])
+    ok_o, rep_o = o.constraints(g_eval[name], g_eval["start"], g_eval["goal"])
+    np.testing.assert_array_equal(rep[7:], rep_o[7:])  # the four predicate flags
+    atol = 5e-3 if name == "alpha0" else 1e-5
+    np.testing.assert_allclose(rep[:7], rep_o[:7], rtol=1e-4, atol=atol)
+
+
+def test_init_trajectory(g_eval):
+    c = ctx()
+    a0 = c.init_alpha(START, GOAL)
+    np.testing.assert_allclose(c.evaluate(a0), g_eval["alpha0_traj"], rtol=0, atol=5e-4)
+    rng = np.random.default_rng(3)
+    s = rng.uniform(-0.5, 0.5, (9, 3)).astype(np.float32)
+    g = rng.uniform(0.2, 1.6, (9, 3)).astype(np.float32)
+    o = oracle_for()
+    A = c.init_alpha(s, g)
+    for b in range(9):
+        np.testing.assert_allclose(c.evaluate(A[b]), o.evaluate(o.init_alpha(s[b], g[b])), rtol=0, atol=5e-4)
+
+
+# ----------------------------------------------------------------- the optimiser
+
+def test_gd_first_iterations(g_gd):
+    for k in range(1, 6):
+        c = ctx("--optimizer-name", "gd", "--max-outer-iteration", 1, "--max-inner-iteration", k)
+        alpha, traj, st = c.optimize(START, GOAL, obstacles(), alpha0=g_gd["alpha0"])
+        assert int(st["grad_evals"]) == k and int(st["inner_iterations"]) == k
+        np.testing.assert_allclose(traj, g_gd[f"traj_{k}"], rtol=0, atol=1e-3)
+        assert abs(float(st["final_loss"]) - float(g_gd[f"loss_{k}"])) <= 2e-4 * abs(float(g_gd[f"loss_{k}"]))
+        # the returned α reproduces the returned trajectory through K@α@J
+        np.testing.assert_allclose(c.evaluate(alpha), traj, rtol=0, atol=1e-3)
+
+
+def test_zero_iterations_return_init_trajectory():
+    """max_inner_iteration = 0: optimize() returns α0 and K·α0·J unchanged (the in-kernel
+    initTrajectory is bit-identical to irm_init_alpha)."""
+    c = ctx("--optimizer-name", "gd", "--max-outer-iteration", 1, "--max-inner-iteration", 0)
+    rng = np.random.default_rng(2)
+    s = rng.uniform(-0.5, 0.5, (7, 3)).astype(np.float32)
+    g = rng.uniform(0.2, 1.6, (7, 3)).astype(np.float32)
+    alpha, traj, st = c.optimize(s, g, obstacles())
+    a0 = c.init_alpha(s, g)
+    np.testing.assert_array_equal(alpha, a0)
+    np.testing.assert_array_equal(traj, c.evaluate(a0))
+    assert np.all(st["grad_evals"] == 0) and np.all(st["outer_iterations"] == 1)
+
+
+def test_gd_single_loop_iteration_count(g_gd):
+    """Reference and oracle both stop the first GD loop after 128 steps."""
+    c = ctx("--optimizer-name", "gd", "--max-outer-iteration", 1)
+    _, _, st = c.optimize(START, GOAL, obstacles(), alpha0=g_gd["alpha0"])
+    assert int(st["grad_evals"]) == 128
+
+
+@pytest.mark.parametrize("tag", sorted(E2E_CASES))
+@pytest.mark.parametrize("rank", [0, -1])
+def test_end_to_end_quality(g_e2e, tag, rank):
+    """Full optimize() at the reference defaults, low-rank (auto) and dense operator."""
+    argv, n_obs = E2E_CASES[tag]
+    c = ctx(*argv, operator_rank=rank)
+    obs = obstacles(n_obs)
+    alpha, traj, st = c.optimize(START, GOAL, obs)
+    avg = c.eval_cost(alpha, obs, START, GOAL, 0, 0, 0)
+    mx = c.eval_cost(alpha, obs, START, GOAL, 0, 0, 1)
+    ok, _ = c.constraints(alpha, START, GOAL)
+    assert bool(st["constraints_ok"]) == ok
+    check_quality(g_e2e, tag, avg, mx, ok)
+    np.testing.assert_allclose(c.evaluate(alpha), traj, rtol=0, atol=2e-3)
+
+
+def test_series_matches_plain_loop_semantics(g_e2e):
+    """--extended-vis: frame 0 = initial trajectory, one frame per accepted step."""
+    c = ctx("--jit-loop", "false", "--extended-vis", "true", record_series=1)
+    alpha, traj, st, ser = c.optimize(START, GOAL, obstacles(), series=True)
+    ref = g_e2e["bls_n50_series__series"]
+    assert len(ser) == int(st["series_len"]) == int(st["inner_iterations"]) + 1
+    np.testing.assert_allclose(ser[0], ref[0], rtol=0, atol=5e-4)
+    np.testing.assert_allclose(ser[1], ref[1], rtol=0, atol=5e-2)
+    np.testing.assert_array_equal(ser[-1], traj)  # last frame = trajectory of the returned α
+
+
+def test_batch_equals_single_and_permutation():
+    """A problem's result does not depend on its batch neighbours: results of a batch equal
+    the single-problem results (tolerance: summation-tile differences), and permuting the
+    batch permutes the results bit for bit."""
+    args = ("--optimizer-name", "gd", "--max-outer-iteration", 1, "--max-inner-iteration", 40)
+    c = ctx(*args)
+    rng = np.random.default_rng(11)
+    B = 21
+    s = rng.uniform(-0.5, 0.5, (B, 3)).astype(np.float32)
+    g = rng.uniform(0.2, 1.6, (B, 3)).astype(np.float32)
+    obs = obstacles()
+    _, traj, st = c.optimize(s, g, obs)
+    perm = rng.permutation(B)
+    _, traj_p, st_p = c.optimize(s[perm], g[perm], obs)
+    np.testing.assert_array_equal(traj_p, traj[perm])
+    for b in (0, 7, 20):
+        _, t1, _ = c.optimize(s[b], g[b], obs)
+        np.testing.assert_allclose(t1, traj[b], rtol=0, atol=1e-4)
+    _, traj2, _ = c.optimize(s, g, obs)
+    np.testing.assert_array_equal(traj2, traj)  # deterministic
+
+
+def _ref64(args):
+    """The reference algorithm in exact (fp64) arithmetic on the reference's fp32 K, dK, J."""
+    from irm_motion_planning_amd.params import params_from_args
+    from oracle.oracle import Oracle
+    from oracle.ref64 import Ref64
+    p = params_from_args(args)
+    o = Oracle(p)
+    _, K, dK, J = o.kernel_matrices()
+    return o, Ref64(p, K, dK, J)
+
+
+def _ref64_band(r, a0, obs, s, g, iters, n_ens=2):
+    """Exact-arithmetic result and its sensitivity: the largest waypoint change when α0 moves
+    by ±1 ulp (the max-cost argmax makes the GD map discontinuous, so nearby starts separate)."""
+    a64, l64, n = r.gd_single(a0, obs, s, g, iters)
+    T64 = r.traj_vel(a64)[0]
+    spread = 0.0
+    for seed in range(n_ens):
+        sgn = np.random.default_rng(100 + seed).choice([-1.0, 1.0], a0.shape).astype(np.float32)
+        ap = np.nextafter(a0, a0 + sgn * np.float32(np.inf)).astype(np.float32)
+        ae, _, _ = r.gd_single(ap, obs, s, g, iters)
+        spread = max(spread, float(np.abs(r.traj_vel(ae)[0] - T64).max()))
+    return T64, l64, n, spread
+
+
+# With λmax > 0 a step whose argmax waypoint differs between fp32 and fp64 (a near-tie of two
+# waypoints' obstacle costs) moves the trajectory by ≈ lr·λmax·|∇cost|·|K| — measured up to
+# 4e-2 after 200 steps (C4 problem 0) while the final loss still agrees to 2e-4.
+ARGMAX_SLACK = 5e-2
+
+
+def _bench_vs_ref(cfg, B, n_check, iters=200, lmax=None, slack=1e-3):
+    """Bench mode (exactly `iters` GD steps per problem) against the reference algorithm in
+    exact (fp64) arithmetic, from the same α0 (the device's initTrajectory).
+
+    Per problem: final loss within 1e-3 (relative) and
+      |traj − exact| ≤ 3·spread + 2·round + slack, where
+      spread — the exact iteration's own change under ±1 ulp on α0 (the max-cost term sends
+               its gradient to the argmax waypoint only, so near-ties separate nearby runs);
+      round  — |K·fp32(α)·J − K·α·J| of the exact α: returning α in fp32 (|α| ≈ 1e3, singular
+               K) moves the trajectory it represents by this much (traj_out is K·α_out·J).
+    (The reference's own fp32 α-space iteration drifts from the exact one by up to ~0.2 here —
+    test_oracle_golden.py::test_fp32_alpha_drift.)"""
+    import bench
+    from irm_motion_planning_amd.context import Context
+    from irm_motion_planning_amd.params import params_from_args
+    args = bench.make_args(cfg, False, iters)
+    if lmax is not None:
+        args.lambda_max_cost = lmax
+    s, g, obs = bench.make_problem(cfg, 1, 0)
+    s, g = s[:B], g[:B]
+    c = Context(params_from_args(args))
+    alpha, traj, st = c.optimize(s, g, obs)
+    assert np.all(st["grad_evals"] == iters) and np.all(np.isfinite(traj))
+    _, r = _ref64(args)
+    for b in np.linspace(0, B - 1, n_check).astype(int):
+        a0 = c.init_alpha(s[b], g[b])
+        T64, l64, n, spread = _ref64_band(r, a0, obs, s[b], g[b], iters)
+        a64, _, _ = r.gd_single(a0, obs, s[b], g[b], iters)
+        rnd = float(np.abs(r.traj_vel(a64.astype(np.float32))[0] - T64).max())
+        err = float(np.abs(traj[b] - T64).max())
+        print(f"{cfg}[{b}] lmax={args.lambda_max_cost} {iters} steps: |traj - exact| {err:.2e}, "
+              f"spread {spread:.2e}, round {rnd:.2e}, loss {float(st['final_loss'][b]):.6f} vs {l64:.6f}")
+        assert n == iters
+        assert err <= 3 * spread + 2 * rnd + slack, (b, err, spread, rnd)
+        assert abs(float(st["final_loss"][b]) - l64) <= 1e-3 * abs(l64)
+    return c, alpha, traj, st
+
+
+@pytest.mark.parametrize("cfg,B", [("c3", 256), ("c4", 32), ("c5", 16)])
+def test_bench_smooth_objective_tracks_exact_iteration(cfg, B):
+    """λmax = 0 (mean obstacle cost only): 200 steps within 2e-3 (+ sensitivity) of exact."""
+    _bench_vs_ref(cfg, B, 4, lmax=0.0)
+
+
+def test_bench_c3_full_size_properties():
+    """BASELINE configs[2] at full size (1024 × N=128): every problem runs exactly 200 GD
+    iterations, K@α_out@J reproduces traj_out bit for bit, results are deterministic, and
+    a spread of problems matches the exact-arithmetic reference."""
+    c, alpha, traj, st = _bench_vs_ref("c3", 1024, 8, slack=ARGMAX_SLACK)
+    import bench
+    np.testing.assert_array_equal(c.evaluate(alpha[::97]), traj[::97])
+    s, g, obs = bench.make_problem("c3", 1, 0)
+    _, traj2, _ = c.optimize(s, g, obs)
+    np.testing.assert_array_equal(traj2, traj)
+
+
+def test_bench_c4_random_obstacles():
+    _bench_vs_ref("c4", 64, 4, slack=ARGMAX_SLACK)
+
+
+def test_bench_c5_seven_dof():
+    _bench_vs_ref("c5", 32, 3, slack=ARGMAX_SLACK)
+
+
+def test_per_problem_obstacles_and_edge_counts():
+    """obstacle_stride > 0: each problem its own obstacle set; also O = 0 and O = 64."""
+    args = ("--optimizer-name", "gd", "--max-outer-iteration", 1, "--max-inner-iteration", 30)
+    c = ctx(*args)
+    from conftest import ref_args
+    o, r = _ref64(ref_args(*args))
+    rng = np.random.default_rng(5)
+    B = 5
+    s = rng.uniform(-0.5, 0.5, (B, 3)).astype(np.float32)
+    g = rng.uniform(0.2, 1.6, (B, 3)).astype(np.float32)
+    for O in (0, 1, 7, 64):
+        obs = rng.uniform(-3.5, 3.5, (B, O, 2)).astype(np.float32)
+        _, traj, st = c.optimize(s, g, obs, obstacle_stride=2 * O)  # stride in floats (irm.h)
+        for b in range(B):
+            a0 = c.init_alpha(s[b], g[b])
+            T64, _, n, spread = _ref64_band(r, a0, obs[b], s[b], g[b], 30)
+            a64, _, _ = r.gd_single(a0, obs[b], s[b], g[b], 30)
+            rnd = float(np.abs(r.traj_vel(a64.astype(np.float32))[0] - T64).max())
+            err = float(np.abs(traj[b] - T64).max())
+            assert err <= 3 * spread + 2 * rnd + 1e-3, (O, b, err, spread, rnd)  # see _bench_vs_ref
+            if spread < 1e-4:  # the loop-exit step is only defined where the iteration is stable
+                assert int(st["grad_evals"][b]) == min(n + 1, 30)
+
+
+def test_device_pointer_entry_point():
+    """irm_optimize_batch_dev on torch-allocated HBM (the bench path) == host entry point."""
+    import torch
+    from irm_motion_planning_amd.context import batch_dev
+    args = ("--optimizer-name", "gd", "--max-outer-iteration", 1, "--max-inner-iteration", 25)
+    c = ctx(*args)
+    rng = np.random.default_rng(9)
+    B = 33
+    s = rng.uniform(-0.5, 0.5, (B, 3)).astype(np.float32)
+    g = rng.uniform(0.2, 1.6, (B, 3)).astype(np.float32)
+    obs = obstacles()
+    alpha_h, traj_h, st_h = c.optimize(s, g, obs)
+    dev = torch.device("cuda", 0)
+    st_t, gl_t, ob_t = (torch.from_numpy(x).to(dev) for x in (s, g, obs))
+    al_t = torch.empty((B, 50, 3), dtype=torch.float32, device=dev)
+    tr_t = torch.empty_like(al_t)
+    ss_t = torch.zeros((B, 8), dtype=torch.int32, device=dev)
+    bd = batch_dev(start=st_t.data_ptr(), goal=gl_t.data_ptr(), obstacles=ob_t.data_ptr(), n_obstacles=11, batch=B,
+                   alpha_out=al_t.data_ptr(), traj_out=tr_t.data_ptr(), stats_out=ss_t.data_ptr())
+    stream = torch.cuda.current_stream(dev)
+    c.optimize_dev(bd, stream.cuda_stream)
+    torch.cuda.synchronize(dev)
+    np.testing.assert_array_equal(tr_t.cpu().numpy(), traj_h)
+    np.testing.assert_array_equal(al_t.cpu().numpy(), alpha_h)
+    np.testing.assert_array_equal(ss_t.cpu().numpy()[:, 2], st_h["grad_evals"])
+
+
+# ----------------------------------------------------------------- drop-in surface
+
+def test_main_cli_writes_reference_files(tmp_path, capsys):
+    """main.py:105-153: stdout lines and trajectory_result.txt / trajectory_series.txt."""
+    from irm_motion_planning_amd import main as irm_main
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        irm_main.main(["--extended-vis", "true", "--n-measurements", "2"])
+    finally:
+        os.chdir(cwd)
+    out = capsys.readouterr().out
+    assert "setup object, jit-compile took" in out and "runtimes in ms: mean" in out
+    assert "result cost: ( avg" in out and "constraint fulfiled True" in out
+    res = np.loadtxt(tmp_path / "trajectory_result.txt")
+    ser = np.loadtxt(tmp_path / "trajectory_series.txt")
+    assert res.shape == (50, 3) and ser.shape[1] == 150 and ser.shape[0] > 10
+    assert np.abs(res[0] - START).max() < 0.01 and np.abs(res[-1] - GOAL).max() < 0.01
+
+
+def test_object_api(g_e2e):
+    """Optimizer(args).optimize() → α; .trajectory / .env as main.py uses them."""
+    from conftest import ref_args
+    from irm_motion_planning_amd.optimizer_BLS import BacktrackingLineSearchOptimizer
+    from irm_motion_planning_amd.optimizer_GD import GradientDescentOptimizer
+    for cls, tag, argv in ((BacktrackingLineSearchOptimizer, "bls_n50_lmax0.5", []),
+                           (GradientDescentOptimizer, "gd_n50", ["--optimizer-name", "gd"])):
+        opt = cls(ref_args(*argv))
+        alpha = opt.optimize()
+        tr, env = opt.trajectory, opt.env
+        assert alpha.shape == (50, 3) and alpha.dtype == np.float32
+        avg = tr.compute_trajectory_cost(alpha, env.obstacles, env.start_config, env.goal_config, 0, 0, 0)
+        mx = tr.compute_trajectory_cost(alpha, env.obstacles, env.start_config, env.goal_config, 0, 0, 1)
+        ok = tr.constraintsFulfilledVerbose(alpha, env.start_config, env.goal_config, verbose=False)
+        check_quality(g_e2e, tag, avg, mx, ok)
+        traj = tr.evaluate(alpha, tr.km, tr.jac)
+        assert traj.shape == (50, 3)
+        g = tr.compute_trajectory_cost_g(alpha, env.obstacles, env.start_config, env.goal_config, 0.5, 0.1, 0.5)
+        assert g.shape == (50, 3) and np.all(np.isfinite(g))

@@ -1,0 +1,226 @@
+"""Pin the CPU oracle (oracle/irm_oracle.c) to the reference's golden vectors.
+
+The golden vectors come from the unmodified reference (gen_golden.py).
+Tolerances follow SURVEY.md §8c.  Where K@α is ill-conditioned (α0 from the
+singular initTrajectory solve, |α| ≈ 1e3), results differ in fp32 noise from
+any two summation orders; the exactness of the arithmetic itself is checked
+at well-conditioned α ("small1", "small2") to ~1e-6.
+"""
+import numpy as np
+import pytest
+
+from conftest import E2E_CASES, GOAL, START, check_quality, obstacles, oracle_for
+
+
+@pytest.mark.parametrize("N", [50, 64, 128, 256])
+def test_kernel_matrices(g_setup, N):
+    """trajectory.py:35-42 — t, K, dK (rtol 1e-6) and J (exact)."""
+    t, K, dK, J = oracle_for("--n-timesteps", N).kernel_matrices()
+    np.testing.assert_array_equal(t, g_setup[f"t_{N}"])
+    if N <= 64:
+        np.testing.assert_allclose(K, g_setup[f"K_{N}"], rtol=1e-6, atol=2e-7)
+        np.testing.assert_allclose(dK, g_setup[f"dK_{N}"], rtol=1e-6, atol=2e-6)
+    else:
+        r = [0, N // 2, N - 1]
+        np.testing.assert_allclose(K[r], g_setup[f"Krows_{N}"], rtol=1e-6, atol=2e-7)
+        np.testing.assert_allclose(dK[r], g_setup[f"dKrows_{N}"], rtol=1e-6, atol=2e-6)
+    np.testing.assert_array_equal(J, g_setup["J"])
+
+
+def test_default_jac_7dof(g_setup):
+    """J = I + 0.15·normal(PRNGKey(0), (7, 7)) (legacy threefry), C5's robot."""
+    from oracle.oracle import default_jac
+    np.testing.assert_allclose(default_jac(7), np.eye(7, dtype=np.float32) + np.float32(0.15) * g_setup["Z7"],
+                               rtol=0, atol=1e-7)
+
+
+@pytest.mark.parametrize("name", ["alpha0", "small1", "small2"])
+def test_evaluate(g_eval, name):
+    """trajectory.py:63-65 — K@α@J and dK@α@J."""
+    o = oracle_for()
+    a = g_eval[name]
+    tol_t, tol_v = (5e-4, 5e-3) if name == "alpha0" else (1e-6, 5e-6)
+    np.testing.assert_allclose(o.evaluate(a, 0), g_eval[name + "_traj"], rtol=0, atol=tol_t)
+    np.testing.assert_allclose(o.evaluate(a, 1), g_eval[name + "_vel"], rtol=0, atol=tol_v)
+
+
+@pytest.mark.parametrize("name", ["small1", "small2"])
+def test_cost_and_grad_exact(g_eval, name):
+    """trajectory.py:271-297 at well-conditioned α: cost rtol 1e-6, grad 1e-6·max|G|."""
+    o = oracle_for()
+    a, obs = g_eval[name], g_eval["obstacles"]
+    for i, lam in enumerate(g_eval["lams"]):
+        c = o.cost(a, obs, g_eval["start"], g_eval["goal"], *lam)
+        g = o.cost_g(a, obs, g_eval["start"], g_eval["goal"], *lam)
+        ref_c, ref_g = g_eval[name + "_cost"][i], g_eval[name + "_grad"][i]
+        assert abs(c - ref_c) <= 1e-6 * abs(ref_c) + 1e-7, (lam, c, ref_c)
+        assert np.abs(g - ref_g).max() <= 1e-6 * np.abs(ref_g).max(), lam
+
+
+def test_cost_and_grad_at_alpha0(g_eval):
+    """At α0 the fp32 velocity noise (~3e-3, see test_evaluate) enters the λ-weighted
+    start/goal-velocity term linearly; cost rtol 2e-4, grad within 1e-3·max|G| when
+    λ_sg = 0 and 0.1·max|G| when λ_sg ≥ 0.5 (50× amplification at λ_sg = 50)."""
+    o = oracle_for()
+    a, obs = g_eval["alpha0"], g_eval["obstacles"]
+    for i, lam in enumerate(g_eval["lams"]):
+        c = o.cost(a, obs, g_eval["start"], g_eval["goal"], *lam)
+        g = o.cost_g(a, obs, g_eval["start"], g_eval["goal"], *lam)
+        ref_c, ref_g = g_eval["alpha0_cost"][i], g_eval["alpha0_grad"][i]
+        assert abs(c - ref_c) <= 2e-4 * abs(ref_c), (lam, c, ref_c)
+        tol = 1e-3 if lam[0] == 0 else 0.1
+        assert np.abs(g - ref_g).max() <= tol * np.abs(ref_g).max(), lam
+
+
+@pytest.mark.parametrize("name", ["alpha0", "small1", "small2"])
+def test_fk_jacobian_potential(g_eval, name):
+    """robot.py:29-36, 75-87; environment.py:46-58."""
+    from oracle.oracle import compute_cost_vg
+    o = oracle_for()
+    traj = g_eval[name + "_traj"]
+    np.testing.assert_allclose(o.fk(traj), g_eval[name + "_fk"], rtol=0, atol=5e-7)
+    np.testing.assert_allclose(o.jacobian(traj), g_eval[name + "_jac"], rtol=0, atol=5e-7)
+    cv, cg = compute_cost_vg(g_eval[name + "_fk"], g_eval["obstacles"])
+    np.testing.assert_allclose(cv, g_eval[name + "_cost_v"], rtol=1e-6, atol=0)
+    np.testing.assert_allclose(cg, g_eval[name + "_cost_g"], rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("name", ["alpha0", "small1", "small2"])
+def test_constraints_flag(g_eval, name):
+    """trajectory.py:129-137."""
+    ok, rep = oracle_for().constraints(g_eval[name], g_eval["start"], g_eval["goal"])
+    assert ok == bool(g_eval[name + "_ok"])
+    assert rep.shape == (11,)
+
+
+def test_init_trajectory(g_eval):
+    """trajectory.py:73-78: α0 = solve(K, line·J⁻¹); compared in waypoint space."""
+    o = oracle_for()
+    a0 = o.init_alpha(START, GOAL)
+    np.testing.assert_allclose(o.evaluate(a0), g_eval["alpha0_traj"], rtol=0, atol=5e-4)
+    # the interpolation endpoints are hit within the fp32 noise of the singular solve
+    t = o.evaluate(a0)
+    assert np.abs(t[0] - START).max() < 1e-3 and np.abs(t[-1] - GOAL).max() < 1e-3
+
+
+def test_gd_first_iterations(g_gd):
+    """optimizer_GD.py:281-310 (jit_optimize): k = 1..5 steps from the same α0, atol 1e-3."""
+    for k in range(1, 6):
+        o = oracle_for("--optimizer-name", "gd", "--max-outer-iteration", 1, "--max-inner-iteration", k)
+        al, st = o.optimize(g_gd["alpha0"], obstacles(), START, GOAL)
+        assert st["grad_evals"] == k and st["inner_iterations"] == k
+        np.testing.assert_allclose(o.evaluate(al), g_gd[f"traj_{k}"], rtol=0, atol=1e-3)
+        assert abs(st["final_loss"] - float(g_gd[f"loss_{k}"])) <= 1e-4 * abs(float(g_gd[f"loss_{k}"]))
+
+
+@pytest.mark.parametrize("tag", sorted(E2E_CASES))
+def test_end_to_end_quality(g_e2e, tag):
+    """Full optimize() (jit loop, default hyper-parameters): avg/max obstacle cost and the
+    constraint flag inside the reference's own ±1-ulp spread (conftest.check_quality)."""
+    argv, n_obs = E2E_CASES[tag]
+    o = oracle_for(*argv)
+    obs = obstacles(n_obs)
+    al, st = o.optimize(o.init_alpha(START, GOAL), obs, START, GOAL)
+    avg = o.cost(al, obs, START, GOAL, 0, 0, 0)
+    mx = o.cost(al, obs, START, GOAL, 0, 0, 1)
+    ok, _ = o.constraints(al, START, GOAL)
+    assert bool(st["constraints_ok"]) == ok
+    check_quality(g_e2e, tag, avg, mx, ok)
+
+
+def test_gd_single_loop_iteration_count(g_gd):
+    """First outer loop of GD is not noise-terminated: 128 iterations in the reference run
+    (gen_golden per-λ counts) — the oracle's single loop stops at the same step."""
+    o = oracle_for("--optimizer-name", "gd", "--max-outer-iteration", 1)
+    _, st = o.optimize(g_gd["alpha0"], obstacles(), START, GOAL)
+    assert st["grad_evals"] == 128
+
+
+def test_series_frames(g_e2e):
+    """optimizer_BLS.py:65-123 (plain loop, extended vis): frame 0 is the initial
+    trajectory; early frames follow the reference before chaos sets in."""
+    o = oracle_for("--jit-loop", "false", "--extended-vis", "true")
+    al, st, ser = o.optimize(o.init_alpha(START, GOAL), obstacles(), START, GOAL, max_series=512)
+    ref = g_e2e["bls_n50_series__series"]
+    assert ser.shape[1:] == ref.shape[1:]
+    assert len(ser) == st["inner_iterations"] + 1
+    np.testing.assert_allclose(ser[0], ref[0], rtol=0, atol=5e-4)
+    np.testing.assert_allclose(ser[1], ref[1], rtol=0, atol=5e-2)
+
+
+def test_reference_visualization_fixture(g_vis):
+    """The reference's committed visualization/trajectory_{result,series}.txt (format and
+    qualitative check): 146 frames of 50×3; frame 0 is the init trajectory."""
+    from oracle.oracle import compute_cost_vg
+    o = oracle_for()
+    assert g_vis["trajectory_result"].shape == (50, 3)
+    assert int(g_vis["series_len"]) == 146
+    frames = g_vis["series_frames"].reshape(-1, 50, 3)
+    np.testing.assert_allclose(frames[0], o.evaluate(o.init_alpha(START, GOAL)), rtol=0, atol=5e-4)
+    res = g_vis["trajectory_result"]
+    cv, _ = compute_cost_vg(o.fk(res), obstacles())
+    assert abs(cv.mean() - 1.69) < 0.03 and abs(cv.max() - 2.19) < 0.03  # blog-post.html:546-581
+
+
+def test_gradient_finite_difference():
+    """the analytic gradient against central differences at a
+    well-conditioned α (fp32 cost, h = 1e-2 on a few entries, 2 % tolerance)."""
+    o = oracle_for()
+    rng = np.random.default_rng(5)
+    a = (rng.standard_normal((50, 3)) * 0.1).astype(np.float32)
+    obs = obstacles()
+    lam = (0.5, 0.1, 0.5)
+    g = o.cost_g(a, obs, START, GOAL, *lam)
+    idx = [(0, 0), (7, 1), (25, 2), (49, 0), (33, 1)]
+    for n, k in idx:
+        ap, am = a.copy(), a.copy()
+        ap[n, k] += 1e-2
+        am[n, k] -= 1e-2
+        fd = (o.cost(ap, obs, START, GOAL, *lam) - o.cost(am, obs, START, GOAL, *lam)) / 2e-2
+        assert abs(fd - g[n, k]) <= 0.02 * np.abs(g).max(), (n, k, fd, g[n, k])
+
+
+def test_ref64_restates_the_oracle():
+    """oracle/ref64.py (fp64 numpy) and the C oracle agree where fp32 is well conditioned."""
+    from oracle.ref64 import Ref64
+    o = oracle_for()
+    _, K, dK, J = o.kernel_matrices()
+    r = Ref64(o.params, K, dK, J)
+    rng = np.random.default_rng(2)
+    a = (rng.standard_normal((50, 3)) * 0.2).astype(np.float32)
+    obs = obstacles()
+    for lam in ((0.5, 0.1, 0.5), (50, 10, 0), (5, 1, 1)):
+        assert abs(r.cost(a, obs, START, GOAL, *lam) - o.cost(a, obs, START, GOAL, *lam)) <= 2e-6 * abs(
+            r.cost(a, obs, START, GOAL, *lam))
+        g64, g32 = r.cost_g(a, obs, START, GOAL, *lam), o.cost_g(a, obs, START, GOAL, *lam)
+        assert np.abs(g64 - g32).max() <= 2e-6 * np.abs(g64).max()
+
+
+def test_fp32_alpha_drift():
+    """The reference iterates α in fp32 with |α| ≈ 1e3 (singular K): every step's rounding of α
+    moves the waypoints by ~5e-4, and over 200 bench-mode GD steps the fp32 iteration drifts
+    from the same iteration in exact arithmetic by O(0.1) (C3 problem 0: 0.19, loss 1.8036 vs
+    1.7906).  The HIP kernel iterates in waypoint space and follows the exact iteration
+    (test_gpu_parity.py::_bench_vs_ref); this records the size of the reference's own drift."""
+    import bench
+    from irm_motion_planning_amd.params import params_from_args
+    from oracle.oracle import Oracle
+    from oracle.ref64 import Ref64
+    s, g, obs = bench.make_problem("c3", 1, 0)
+    p = params_from_args(bench.make_args("c3", False, 200))
+    o = Oracle(p)
+    _, K, dK, J = o.kernel_matrices()
+    r = Ref64(p, K, dK, J)
+    a0 = o.init_alpha(s[0], g[0])
+    a32, st = o.optimize(a0, obs, s[0], g[0])
+    a64, l64, n = r.gd_single(a0, obs, s[0], g[0], 200)
+    drift = np.abs(o.evaluate(a32) - r.traj_vel(a64)[0]).max()
+    assert n == 200 and st["grad_evals"] == 200
+    assert 0.05 < drift < 0.5, drift
+    assert l64 < st["final_loss"]  # the exact iteration reaches the lower loss
+    # one step: the drift is the rounding of α alone
+    p1 = params_from_args(bench.make_args("c3", False, 1))
+    o1 = Oracle(p1)
+    a32, _ = o1.optimize(a0, obs, s[0], g[0])
+    a64, _, _ = r.gd_single(a0, obs, s[0], g[0], 1)
+    assert np.abs(o1.evaluate(a32) - r.traj_vel(a64)[0]).max() < 2e-3

@@ -67,7 +67,58 @@ def check(opt, N=50, rank=0, extra=()):
              f" orc {orc.cost(ao, env.obstacles, env.start_config, env.goal_config, 0, 0, lm):.5f}")
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and len(sys.argv) == 1:
     for opt in ("gd", "bls"):
         for N, rank in ((50, 0), (50, -1), (128, 0)):
             check(opt, N, rank)
+
+
+def bench_drift(cfg="c3", probs=(0, 146, 292), iters=(1, 5, 20, 50, 100, 200), ranks=(0, -1)):
+    """Bench-mode GD (fixed iterations): GPU vs oracle per iteration count."""
+    import bench
+    s, g, obs = bench.make_problem(cfg, 1, 0)
+    for rank in ranks:
+        for it in iters:
+            args = bench.make_args(cfg, False, it)
+            p = params_from_args(args, operator_rank=rank)
+            ctx, orc = Context(p), Oracle(p)
+            diffs = []
+            for b in probs:
+                a0 = orc.init_alpha(s[b], g[b])
+                _, traj, st = ctx.optimize(s[b], g[b], obs, alpha0=a0)
+                ao, sto = orc.optimize(a0, obs, s[b], g[b])
+                diffs.append(f"{np.abs(traj - orc.evaluate(ao)).max():.2e}/{float(st['final_loss']) - sto['final_loss']:+.1e}")
+            line(f"  {cfg} rank={rank} iters={it}: traj diff / loss diff per problem: {diffs}")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "drift":
+    bench_drift()
+
+
+def exact_drift(cfg="c3", b=0, iters=(1, 2, 3, 5, 10, 20), ranks=(0, -1), lmaxs=(0.0, 0.5)):
+    """GPU vs the reference algorithm in fp64 (oracle/ref64.py), per iteration count."""
+    import bench
+    from oracle.ref64 import Ref64
+    s, g, obs = bench.make_problem(cfg, 1, 0)
+    for lmax in lmaxs:
+        for rank in ranks:
+            for it in iters:
+                args = bench.make_args(cfg, False, it)
+                args.lambda_max_cost = lmax
+                p = params_from_args(args, operator_rank=rank)
+                ctx, orc = Context(p), Oracle(p)
+                _, K, dK, J = orc.kernel_matrices()
+                r = Ref64(p, K, dK, J)
+                a0 = orc.init_alpha(s[b], g[b])
+                _, traj, st = ctx.optimize(s[b], g[b], obs, alpha0=a0)
+                a64, l64, n = r.gd_single(a0, obs, s[b], g[b], it)
+                T64, V64 = r.traj_vel(a64)
+                d = np.abs(traj - T64)
+                i = np.unravel_index(np.argmax(d), d.shape)
+                line(f"  {cfg}[{b}] lmax={lmax} rank={rank} it={it}: |T-T64| {d.max():.2e} at {i}, "
+                     f"loss {float(st['final_loss']):.7f} vs {l64:.7f}")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "exact":
+    exact_drift()
+    exact_drift("c4", 0, iters=(1, 5, 20), ranks=(0,), lmaxs=(0.0,))
