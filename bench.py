@@ -120,6 +120,19 @@ def cpu_baseline(cfg, args, start, goal, obstacles, budget_s=12.0):
                       f"{dt:.2f} s wall on {cores} threads); 1-thread rate {st1[0]['grad_evals'] / t1:.1f} it/s"}
 
 
+def pmc_traffic(cfg):
+    """HBM bytes per k_optimize launch from the newest profiles/*_pmc.json (rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes of this bench command, tools/profile_round.sh), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc.json")))
+    for path in reversed(files):
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("config", "c3") == cfg and d.get("hbm_bytes_per_launch"):
+            return float(d["hbm_bytes_per_launch"]), os.path.relpath(path, HERE)
+    return None, None
+
+
 def share_environment(obs_t, world):
     """Rank 0's obstacles to every rank (RCCL broadcast over xGMI; gloo in the CPU tests)."""
     if world > 1:
@@ -216,6 +229,7 @@ def main():
     launch_flops = exec_f * iters_rank
     achieved = launch_flops / (kernel_ms * 1e-3) / 1e12
     bytes_launch = B * (2 * D + 2 * N * D) * 4 + B * 32  # start/goal in; alpha/traj/stats out
+    traffic, traffic_src = pmc_traffic(a.config) if (a.max_inner == 200 and not a.faithful) else (None, None)
     result = {
         "metric": "GD iterations/sec (batch of trajectories)",
         "value": value,
@@ -243,7 +257,8 @@ def main():
             "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved / PEAK_FP32_TFLOPS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_source": traffic_src,
             "kernel": "irm::k_optimize (fp32 MFMA 16x16x4 + VALU)",
             "kernel_ms": kernel_ms,
             "flops_per_iteration": exec_f,

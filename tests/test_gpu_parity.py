@@ -239,13 +239,14 @@ def _ref64_band(r, a0, obs, s, g, iters, n_ens=2):
     by ±1 ulp (the max-cost argmax makes the GD map discontinuous, so nearby starts separate)."""
     a64, l64, n = r.gd_single(a0, obs, s, g, iters)
     T64 = r.traj_vel(a64)[0]
-    spread = 0.0
+    spread = lspread = 0.0
     for seed in range(n_ens):
         sgn = np.random.default_rng(100 + seed).choice([-1.0, 1.0], a0.shape).astype(np.float32)
         ap = np.nextafter(a0, a0 + sgn * np.float32(np.inf)).astype(np.float32)
-        ae, _, _ = r.gd_single(ap, obs, s, g, iters)
+        ae, le, _ = r.gd_single(ap, obs, s, g, iters)
         spread = max(spread, float(np.abs(r.traj_vel(ae)[0] - T64).max()))
-    return T64, l64, n, spread
+        lspread = max(lspread, abs(le - l64))
+    return T64, l64, n, spread, lspread
 
 
 # With λmax > 0 a step whose argmax waypoint differs between fp32 and fp64 (a near-tie of two
@@ -280,7 +281,7 @@ def _bench_vs_ref(cfg, B, n_check, iters=200, lmax=None, slack=1e-3):
     _, r = _ref64(args)
     for b in np.linspace(0, B - 1, n_check).astype(int):
         a0 = c.init_alpha(s[b], g[b])
-        T64, l64, n, spread = _ref64_band(r, a0, obs, s[b], g[b], iters)
+        T64, l64, n, spread, lspread = _ref64_band(r, a0, obs, s[b], g[b], iters)
         a64, _, _ = r.gd_single(a0, obs, s[b], g[b], iters)
         rnd = float(np.abs(r.traj_vel(a64.astype(np.float32))[0] - T64).max())
         err = float(np.abs(traj[b] - T64).max())
@@ -288,7 +289,7 @@ def _bench_vs_ref(cfg, B, n_check, iters=200, lmax=None, slack=1e-3):
               f"spread {spread:.2e}, round {rnd:.2e}, loss {float(st['final_loss'][b]):.6f} vs {l64:.6f}")
         assert n == iters
         assert err <= 3 * spread + 2 * rnd + slack, (b, err, spread, rnd)
-        assert abs(float(st["final_loss"][b]) - l64) <= 1e-3 * abs(l64)
+        assert abs(float(st["final_loss"][b]) - l64) <= 1e-3 * abs(l64) + 3 * lspread
     return c, alpha, traj, st
 
 
@@ -333,7 +334,7 @@ def test_per_problem_obstacles_and_edge_counts():
         _, traj, st = c.optimize(s, g, obs, obstacle_stride=2 * O)  # stride in floats (irm.h)
         for b in range(B):
             a0 = c.init_alpha(s[b], g[b])
-            T64, _, n, spread = _ref64_band(r, a0, obs[b], s[b], g[b], 30)
+            T64, _, n, spread, _ = _ref64_band(r, a0, obs[b], s[b], g[b], 30)
             a64, _, _ = r.gd_single(a0, obs[b], s[b], g[b], 30)
             rnd = float(np.abs(r.traj_vel(a64.astype(np.float32))[0] - T64).max())
             err = float(np.abs(traj[b] - T64).max())
