@@ -168,7 +168,7 @@ struct irm_ctx {
     KParams kp{};
     // device
     float *d_K = nullptr, *d_dK = nullptr, *d_Kt = nullptr, *d_dKt = nullptr, *d_F1 = nullptr, *d_F2 = nullptr,
-          *d_Fbot = nullptr, *d_Vr = nullptr, *d_Vfrag = nullptr, *d_u = nullptr, *d_w = nullptr;
+          *d_Fbot = nullptr, *d_Vr = nullptr, *d_H = nullptr, *d_u = nullptr, *d_w = nullptr;
     // host-API staging
     void* d_io = nullptr;
     size_t io_bytes = 0;
@@ -219,8 +219,7 @@ int choose_shape(const irm_ctx* c, int B, bool optimizer, KParams& kp, int* lds_
     for (; tb >= 1; --tb) {
         kp.TB = tb;
         kp.BT = tb * kp.NW;
-        const int nw = kp.BT / 64, MT1 = kp.RP / 16, KQ1 = kp.MP / 16;
-        kp.nsplit = std::max(1, std::min(KQ1, nw / std::max(1, MT1)));
+        kp.nsplit = irm::stage1_splits(kp.NK);
         if (optimizer) {
             kp.regops = irm::regops_fit(kp) ? 1 : 0;
             irm::Plan a = irm::plan_lds(kp, true, true);
@@ -381,7 +380,8 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
     c->J.assign(p->jac, p->jac + (size_t)D * D);
 
     // ---- operator factorisation F = L·V_R
-    const int NK = round_up(N, 16), MP = round_up(2 * N, 16);
+    // optimiser row layout: position half rows 0..N-1, velocity half from row NK
+    const int NK = round_up(N, 16), MP = 2 * NK;
     std::vector<double> Ld((size_t)2 * N * N);
     for (int i = 0; i < N; ++i)
         for (int j = 0; j < N; ++j) {
@@ -455,14 +455,16 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
         rc |= upload(&c->d_Kt, kt);
         rc |= upload(&c->d_dKt, dkt);
     }
+    // F rows m < N (K part) → row m, m = N + j (dK part) → row NK + j
+    auto frow = [&](int m) { return m < N ? m : NK + (m - N); };
     A.assign((size_t)RP * MP, 0.0);  // Fᵀ (RP × MP): stage 1 contracts y = Fᵀ·[a; b]
     for (int m = 0; m < 2 * N; ++m)
-        for (int r = 0; r < RP; ++r) A[(size_t)r * MP + m] = F[(size_t)m * RP + r];
+        for (int r = 0; r < RP; ++r) A[(size_t)r * MP + frow(m)] = F[(size_t)m * RP + r];
     fill_frag(frag, RP, MP, A);
     rc |= upload(&c->d_F1, frag);
     A.assign((size_t)MP * RP, 0.0);  // F (MP × RP)
     for (int m = 0; m < 2 * N; ++m)
-        for (int r = 0; r < RP; ++r) A[(size_t)m * RP + r] = F[(size_t)m * RP + r];
+        for (int r = 0; r < RP; ++r) A[(size_t)frow(m) * RP + r] = F[(size_t)m * RP + r];
     fill_frag(frag, MP, RP, A);
     rc |= upload(&c->d_F2, frag);
     std::vector<float> fb((size_t)N * RP), vr((size_t)N * RP);
@@ -473,11 +475,18 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
         }
     rc |= upload(&c->d_Fbot, fb);
     rc |= upload(&c->d_Vr, vr);
-    A.assign((size_t)NK * RP, 0.0);  // V_R (NK × RP), rows ≥ N zero
-    for (int n = 0; n < N; ++n)
-        for (int r = 0; r < RP; ++r) A[(size_t)n * RP + r] = Vd[(size_t)n * RP + r];
-    fill_frag(frag, NK, RP, A);
-    rc |= upload(&c->d_Vfrag, frag);
+    {  // h_e = F·F[N+e]ᵀ for the endpoint velocity rows e ∈ {0, N−1}, kernel row layout
+        std::vector<float> h((size_t)2 * MP, 0.f);
+        for (int e = 0; e < 2; ++e) {
+            const int me = N + (e ? N - 1 : 0);
+            for (int m = 0; m < 2 * N; ++m) {
+                double acc = 0.0;
+                for (int r = 0; r < RP; ++r) acc += F[(size_t)m * RP + r] * F[(size_t)me * RP + r];
+                h[(size_t)e * MP + frow(m)] = (float)acc;
+            }
+        }
+        rc |= upload(&c->d_H, h);
+    }
     // initTrajectory basis: u = K⁻¹(1−c), w = K⁻¹c (fp32 LU, trajectory.py:77)
     {
         std::vector<float> rhs((size_t)N * 2), X((size_t)N * 2);
@@ -567,11 +576,41 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
             irm_ctx_destroy(c);
             return fail(IRM_EINVAL, "J is singular");
         }
-        for (int a = 0; a < D; ++a) {
-            double u = 0.0;
-            for (int i = 0; i < D; ++i) u += (double)p->jac[(size_t)i * D + a];
-            kp.Jcol[a] = (float)u;
+        // (JᵀJ)⁻¹ by Gauss-Jordan in fp64, and w = (JᵀJ)⁻¹·Jᵀ1 (BLS norms from y' = y·JᵀJ)
+        std::vector<double> Mi((size_t)D * D, 0.0), Mw(JtJ);
+        for (int i = 0; i < D; ++i) Mi[(size_t)i * D + i] = 1.0;
+        for (int col = 0; col < D; ++col) {
+            int piv = col;
+            for (int r = col + 1; r < D; ++r)
+                if (std::fabs(Mw[(size_t)r * D + col]) > std::fabs(Mw[(size_t)piv * D + col])) piv = r;
+            for (int k = 0; k < D; ++k) {
+                std::swap(Mw[(size_t)col * D + k], Mw[(size_t)piv * D + k]);
+                std::swap(Mi[(size_t)col * D + k], Mi[(size_t)piv * D + k]);
+            }
+            const double d = Mw[(size_t)col * D + col];
+            for (int k = 0; k < D; ++k) {
+                Mw[(size_t)col * D + k] /= d;
+                Mi[(size_t)col * D + k] /= d;
+            }
+            for (int r = 0; r < D; ++r) {
+                if (r == col) continue;
+                const double f = Mw[(size_t)r * D + col];
+                for (int k = 0; k < D; ++k) {
+                    Mw[(size_t)r * D + k] -= f * Mw[(size_t)col * D + k];
+                    Mi[(size_t)r * D + k] -= f * Mi[(size_t)col * D + k];
+                }
+            }
         }
+        for (int a = 0; a < D; ++a) {
+            double w = 0.0;
+            for (int b = 0; b < D; ++b) {
+                double u = 0.0;
+                for (int i = 0; i < D; ++i) u += (double)p->jac[(size_t)i * D + b];
+                w += Mi[(size_t)a * D + b] * u;
+            }
+            kp.wal[a] = (float)w;
+        }
+        for (int i = 0; i < D * D; ++i) kp.Minv[i] = (float)Mi[i];
         for (int i = 0; i < D * D; ++i) {
             kp.J[i] = p->jac[i];
             kp.JtJ[i] = (float)JtJ[i];
@@ -586,7 +625,7 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
     kp.F2frag = c->d_F2;
     kp.Fbot = c->d_Fbot;
     kp.Vr = c->d_Vr;
-    kp.Vfrag = c->d_Vfrag;
+    kp.Hend = c->d_H;
     kp.uvec = c->d_u;
     kp.wvec = c->d_w;
     kp.lam_max = p->lambda_max_cost;
@@ -617,7 +656,7 @@ void irm_ctx_destroy(irm_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->p.device);
     float* bufs[] = {c->d_K, c->d_dK, c->d_Kt, c->d_dKt, c->d_F1,   c->d_F2,
-                     c->d_Fbot, c->d_Vr, c->d_Vfrag, c->d_u, c->d_w};
+                     c->d_Fbot, c->d_Vr, c->d_H, c->d_u, c->d_w};
     for (float* b : bufs)
         if (b) (void)hipFree(b);
     if (c->d_io) (void)hipFree(c->d_io);

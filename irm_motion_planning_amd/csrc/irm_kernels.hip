@@ -32,39 +32,29 @@ namespace irm {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------ LDS planning
-__host__ __device__ static inline int al4(int x) { return (x + 3) & ~3; }
 
 __host__ __device__ Plan plan_lds(const KParams& p, bool ops_lds, bool optimizer) {
+    const Head H = plan_head(p.MP, p.RP, p.nsplit, optimizer);
     Plan L{};
-    int off = 0;
-    auto take = [&](int n) {
-        int o = off;
-        off += al4(n);
-        return o;
-    };
-    const int N = p.N, TB = p.TB, nw = p.BT / 64;
-    L.f1 = L.f2 = L.fb = 0;
+    L.X = H.X;
+    L.Bs = L.X + p.NK * kLd;
+    L.dP = H.dP;
+    L.Ypart = H.Ypart;
+    L.Ymix = H.Ymix;
+    L.Ydir = L.Yacc = L.alist = L.acnt = L.act = L.list = L.fb = 0;
+    L.red = H.red;
+    L.sg = H.sg;
+    L.wp = H.wp;
+    L.flags = H.flags;
+    L.obs = H.obs;
+    int off = H.obs + al4((p.obs_stride ? p.TB : 1) * ((p.O + 3) & ~3) * 2 + 4);
+    L.f1 = L.f2 = 0;
     if (optimizer && ops_lds && !p.regops) {  // with REGOPS the A-fragments live in VGPRs
-        L.f1 = take((int)frag_floats(p.RP, p.MP));
-        L.f2 = take((int)frag_floats(p.MP, p.RP));
+        L.f1 = off;
+        off += al4((int)frag_floats(p.RP, p.MP));
+        L.f2 = off;
+        off += al4((int)frag_floats(p.MP, p.RP));
     }
-    L.X = take(p.MP * kLd);  // [a; b] stacked: rows 0..N-1 = a, N..2N-1 = b
-    L.Bs = L.X + N * kLd;
-    L.dP = take(p.MP * kLd);
-    L.Ydir = L.Yacc = 0;
-    if (optimizer) {
-        L.Ypart = take(p.nsplit * p.RP * kLd);
-        L.Ymix = take(p.RP * kLd);
-    } else {
-        L.Ypart = L.Ymix = 0;
-    }
-    L.alist = L.acnt = 0;
-    L.red = take(nw * 10);
-    L.sg = take(TB * 4);
-    L.wp = take(nw * 2);
-    L.flags = take(8);
-    L.act = L.list = 0;
-    L.obs = take((p.obs_stride ? TB : 1) * ((p.O + 3) & ~3) * 2 + 4);
     L.total = off;
     return L;
 }
@@ -475,13 +465,14 @@ __device__ void stage_alpha(const KParams& P, int tb0, int ntb, float* X, int xr
 // Lane n of trajectory column block Xa (LDS, rows m = 0..N-1, stride kLd):
 //   q = fp32(fp32(K·α)[n]·J), v = fp32(fp32(dK·α)[n]·J).
 template <int D>
-__device__ void eval_exact(const KParams& P, const float* __restrict__ Xa, int n, float (&q)[D], float (&v)[D]) {
+__device__ void eval_exact(const KParams& P, const float* __restrict__ Xa, int n, float (&q)[D], float (&v)[D],
+                           const float* Kt = nullptr, const float* dKt = nullptr) {
     const int N = P.N;
     double aq[D], av[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) aq[d] = av[d] = 0.0;
-    const float* kt = P.Kt + n;
-    const float* dkt = P.dKt + n;
+    const float* kt = (Kt ? Kt : P.Kt) + n;
+    const float* dkt = (dKt ? dKt : P.dKt) + n;
     for (int m = 0; m < N; ++m) {
         const double kq = (double)kt[(size_t)m * N], kv = (double)dkt[(size_t)m * N];  // K[n][m], dK[n][m]
         const float* xr = Xa + m * kLd;
@@ -545,74 +536,97 @@ __device__ void grad_exact(const KParams& P, const float* __restrict__ Xa, int n
 }
 
 // ------------------------------------------------------------ optimiser
-// Interleaved wave reduction of one evaluation's per-waypoint terms.
+// Wave reduction of one evaluation's per-waypoint terms.
 // usum: Σ_n [(1−λmax)/N·cost_v[n] + λjl/N·(jp[n] + jv[n])], the mean-obstacle and
-// joint-limit terms of trajectory.py:281 folded into one sum.
-struct EvalRed {
-    float cmax;
-    int cidx;
-    float usum, tx, tn, va;
-};
-template <int C>
-__device__ __forceinline__ void ered_step(EvalRed& r) {
-    const float ov = dppf<C>(r.cmax);
-    const int oi = dppi<C>(r.cidx);
-    const float s1 = dppf<C>(r.usum);
-    const float m1 = dppf<C>(r.tx), m2 = dppf<C>(r.tn), m3 = dppf<C>(r.va);
-    amax_step(r.cmax, r.cidx, ov, oi);
-    r.usum += s1;
-    r.tx = fmaxf(r.tx, m1);
-    r.tn = fminf(r.tn, m2);
-    r.va = fmaxf(r.va, m3);
-}
-// Reduce within the wave; lane 0 stores the partial record at red[wave].
-__device__ __forceinline__ void ered_store(EvalRed r, float* red, int wave) {
-    ered_step<0xB1>(r);
-    ered_step<0x4E>(r);
-    ered_step<0x141>(r);
-    ered_step<0x140>(r);
-    EvalRed o;
-    o.cmax = lanef(r.cmax, 0);
-    o.cidx = __builtin_amdgcn_readlane(r.cidx, 0);
-    o.usum = lanef(r.usum, 0);
-    o.tx = lanef(r.tx, 0);
-    o.tn = lanef(r.tn, 0);
-    o.va = lanef(r.va, 0);
-#pragma unroll
-    for (int l = 16; l < 64; l += 16) {
-        amax_step(o.cmax, o.cidx, lanef(r.cmax, l), __builtin_amdgcn_readlane(r.cidx, l));
-        o.usum += lanef(r.usum, l);
-        o.tx = fmaxf(o.tx, lanef(r.tx, l));
-        o.tn = fminf(o.tn, lanef(r.tn, l));
-        o.va = fmaxf(o.va, lanef(r.va, l));
+// joint-limit terms of trajectory.py:281 folded into one sum; cmax with the
+// first-index argmax of jnp.argmax (trajectory.py:97) from a ballot of the lanes
+// holding the wave maximum.  tx/tn/va (constraint extrema) only when `ext`.
+// Lane 0 stores the wave's record at red[wave·8].
+__device__ __forceinline__ void ered_store(bool live, float cv, float us, float tx, float tn, float va, bool ext,
+                                           int n0, float* red, int wave) {
+    float m = live ? cv : -INFINITY, s = live ? us : 0.f;
+    m = fmaxf(m, dppf<0xB1>(m));
+    s += dppf<0xB1>(s);
+    m = fmaxf(m, dppf<0x4E>(m));
+    s += dppf<0x4E>(s);
+    m = fmaxf(m, dppf<0x141>(m));
+    s += dppf<0x141>(s);
+    m = fmaxf(m, dppf<0x140>(m));
+    s += dppf<0x140>(s);
+    const float wm = fmaxf(fmaxf(lanef(m, 0), lanef(m, 16)), fmaxf(lanef(m, 32), lanef(m, 48)));
+    const float ws = (lanef(s, 0) + lanef(s, 16)) + (lanef(s, 32) + lanef(s, 48));
+    const unsigned long long hit = __ballot(live && cv == wm);
+    const int idx = hit ? n0 + __builtin_ctzll(hit) : 0x7fffffff;
+    float ox = 0.f, on = 0.f, oa = 0.f;
+    if (ext) {
+        ox = wred_max(live ? tx : -INFINITY);
+        on = wred_min(live ? tn : INFINITY);
+        oa = wred_max(live ? va : 0.f);
     }
     if ((threadIdx.x & 63) == 0) {
-        float* q = red + wave * 10;
-        q[0] = o.cmax;
-        q[1] = __int_as_float(o.cidx);
-        q[2] = o.usum;
-        q[3] = o.tx;
-        q[4] = o.tn;
-        q[5] = o.va;
+        float* q = red + wave * 8;
+        q[0] = wm;
+        q[1] = __int_as_float(idx);
+        q[2] = ws;
+        q[3] = ox;
+        q[4] = on;
+        q[5] = oa;
     }
 }
 
 // Operator fragments a wave keeps in VGPRs across all rounds (REGOPS).
-constexpr int kS1Q(int maxt) { return maxt <= 256 ? 8 : 4; }   // stage-1 float4 per wave
-constexpr int kS2T(int maxt) { return maxt <= 256 ? 8 : 4; }   // stage-2 tiles per wave (KQ2 ≤ 2)
+// Capacities mirror regops_fit (irm_kernels.hpp): a 512-thread workgroup (8 waves) keeps 4 stage-1
+// k-quads and 2 stage-2 tiles per wave (N ≤ 128 at R = 32), a 256-thread one up to 8 of each.
 
-template <int D, int MAXT, bool OPS_LDS, bool REGOPS>
+// Problem shape of an optimiser launch.  FixShape: compile-time N / R (and everything derived,
+// incl. the LDS layout head) for the common shapes; DynShape: any shape, read from KParams.
+template <int D_, int N_, int RP_>
+struct FixShape {
+    static constexpr int D = D_, N = N_, NK = (N_ + 15) / 16 * 16, MP = 2 * NK, RP = RP_;
+    static constexpr int NW = (N_ + 63) / 64 * 64, WPT = NW / 64, NSPLIT = stage1_splits(NK);
+    __device__ explicit FixShape(const KParams&) {}
+};
+template <int D_>
+struct DynShape {
+    static constexpr int D = D_;
+    int N, NK, MP, RP, NW, WPT, NSPLIT;
+    __device__ explicit DynShape(const KParams& P)
+        : N(P.N), NK(P.NK), MP(P.MP), RP(P.RP), NW(P.NW), WPT(P.NW >> 6), NSPLIT(P.nsplit) {}
+};
+constexpr int kS1Q(int maxt) { return maxt <= 256 ? 8 : 4; }   // stage-1 float4 per wave
+constexpr int kS2T(int maxt) { return maxt <= 256 ? 8 : 2; }   // stage-2 tiles per wave (KQ2 ≤ 2)
+
+// Row layout of the optimiser's [a; b] / [T; V] buffers and of F: the velocity
+// half starts at row NK (= N rounded up to 16), so the position half is whole
+// k-quads of its own and stage 1 can skip the velocity half when b is zero
+// away from the two endpoint rows (the usual case); the endpoint rows then enter
+// through the precomputed operator columns h0 = F·F[NK]ᵀ, h1 = F·F[NK+N−1]ᵀ.
+//
+// One round of a workgroup (TB trajectories, one lane per waypoint):
+//   stage 1   y' = Fᵀ·[a'; b']          (MFMA, split-K over the waves → Ypart)
+//             a' = a·JᵀJ, b' = b·JᵀJ were mixed per lane when written, so y' = y·JᵀJ
+//   stage 2   Δ[T; V] = F·y'            (MFMA; B operand = Σ partials, summed on load)
+//   update    [T; V]' = c·[T; V] − s·Δ  (Δ latched in registers per direction)
+//   evaluate  cost at the trial point; gradient inputs for the next direction
+//   decide    the reference's accept / reject / λ logic per trajectory
+// α is not carried: each lane accumulates the gradient inputs of the accepted
+// steps (acc = c·acc + s·[a'; b']), and α = cprod·α_base − V_R·Fᵀ·acc·J⁻¹ is
+// formed only when an inner loop ends (PH_RESYNC).
+template <class S, int MAXT, bool OPS_LDS, bool REGOPS, bool BLS>
 __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
+    constexpr int D = S::D;
     constexpr int S1Q = kS1Q(MAXT), S2T = kS2T(MAXT);
     extern __shared__ __attribute__((aligned(16))) float smem[];
-    const Plan L = plan_lds(P, OPS_LDS, true);
+    const S sh(P);
+    const Head H = plan_head(sh.MP, sh.RP, sh.NSPLIT, true);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nwaves = P.BT >> 6;
-    const int N = P.N, NW = P.NW, TB = P.TB, RP = P.RP, MP = P.MP, NK = P.NK;
-    const int WPT = NW >> 6;            // waves per trajectory
+    const int N = sh.N, NW = sh.NW, TB = P.TB, RP = sh.RP, MP = sh.MP, NK = sh.NK;
+    const int WPT = sh.WPT;             // waves per trajectory
     const int t = wave / WPT;           // this lane's trajectory (wave-uniform)
     const int n = tid - t * NW;         // this lane's waypoint (and row r of y for n < RP)
+    const int n0 = (wave - t * WPT) * 64;  // first waypoint of this wave
     const int tb0 = blockIdx.x * TB;
     const int ntb = min(TB, P.B - tb0);
     if (ntb <= 0) return;
@@ -620,34 +634,36 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
     const bool valid = tvalid && n < N;
     const bool yrow = tvalid && n < RP;
     const size_t b = (size_t)(tb0 + (tvalid ? t : 0));
-    const bool bls = (P.optimizer == IRM_OPT_BLS);
+    constexpr bool bls = BLS;
     const bool rec = P.record_series && P.series;
     Prof prof;
     if (tid == 0) prof.init();
 
-    float* X = smem + L.X;
-    float* Bs = smem + L.Bs;
-    float* dP = smem + L.dP;
-    float* Ypart = smem + L.Ypart;
-    float* Ymix = smem + L.Ymix;
-    float* red = smem + L.red;
-    float* sg = smem + L.sg;
-    float* wp = smem + L.wp;
-    unsigned* flagw = reinterpret_cast<unsigned*>(smem + L.flags);  // [0,1] dir masks, [2] done mask
-    float* obsL = smem + L.obs;
+    float* X = smem + H.X;    // [a'; b'] (rows 0..N-1, NK..NK+N-1) × 16 columns
+    float* dP = smem + H.dP;  // Δ[T; V], same row layout
+    float* Ypart = smem + H.Ypart;
+    float* Ymix = smem + H.Ymix;
+    float* red = smem + H.red;
+    float* sg = smem + H.sg;
+    float* wp = smem + H.wp;
+    // [0,1] direction masks (bit per column) and [3,4] resync masks (bit per trajectory) by
+    // round parity; [2] done mask; [5,6] "b' non-zero away from the endpoints" by round parity
+    unsigned* flagw = reinterpret_cast<unsigned*>(smem + H.flags);
+    float* obsL = smem + H.obs;
     const float* F1 = P.F1frag;
     const float* F2 = P.F2frag;
 
-    const int KQ1 = MP / 16, MT1 = RP / 16;   // stage 1: (RP × MP)·(MP × 16), K over [a; b]
-    const int KQ2 = RP / 16, MT2 = MP / 16;   // stage 2: (MP × RP)·(RP × 16)
-    const int nsplit = P.nsplit;
-    // stage-1 unit of this wave (split-K): tile u1 % MT1, k-quads [kq0, kq1)
+    const int KQ1 = MP / 16, KQa = NK / 16, MT1 = RP / 16;  // stage 1: (RP × MP)·(MP × 16)
+    const int KQ2 = RP / 16, MT2 = MP / 16;                 // stage 2: (MP × RP)·(RP × 16)
+    const int nsplit = sh.NSPLIT;
+    // stage-1 unit of this wave (split-K over the position half): tile, k-quads [kq0, kq1)
     const bool has1 = wave < MT1 * nsplit;
     const int tile1 = wave % MT1, sp1 = wave / MT1;
-    const int kq0 = (KQ1 * sp1) / nsplit, kq1 = (KQ1 * (sp1 + 1)) / nsplit;
+    const int kq0 = (KQa * sp1) / nsplit, kq1 = (KQa * (sp1 + 1)) / nsplit;
 
     // ----------------------------------------------------------- prologue
     if (OPS_LDS && !REGOPS) {
+        const Plan L = plan_lds(P, OPS_LDS, true);
         const int n1 = (int)frag_floats(RP, MP) / 4, n2 = (int)frag_floats(MP, RP) / 4;
         const f32x4* g1 = reinterpret_cast<const f32x4*>(P.F1frag);
         const f32x4* g2 = reinterpret_cast<const f32x4*>(P.F2frag);
@@ -676,23 +692,59 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                 if (tile < MT2 && i < KQ2) a2[j * 2 + i] = g2[((size_t)tile * KQ2 + i) * 64 + lane];
             }
     }
+    // endpoint-velocity operator columns for this lane's rows (sparse stage 1), and the
+    // F rows of the two endpoint velocities for the BLS norms (rows r = n < RP)
+    const float h0T = valid ? P.Hend[n] : 0.f, h1T = valid ? P.Hend[MP + n] : 0.f;
+    const float h0V = valid ? P.Hend[NK + n] : 0.f, h1V = valid ? P.Hend[MP + NK + n] : 0.f;
+    const float fb0 = yrow ? P.Fbot[(size_t)0 * RP + n] : 0.f;
+    const float fb1 = yrow ? P.Fbot[(size_t)(N - 1) * RP + n] : 0.f;
     stage_obstacles(P, tb0, ntb, obsL);
     for (int e = tid; e < RP * kLd; e += P.BT) Ymix[e] = 0.f;
-    if (tid == 0) {
-        flagw[0] = flagw[1] = 0u;  // direction masks (bit per column), by round parity
-        flagw[2] = 0u;             // done mask (bit per trajectory)
-        flagw[3] = flagw[4] = 0u;  // resync masks (bit per trajectory), by round parity
+    if (tid < 8) flagw[tid] = 0u;
+    // Parameters used only on rare paths (outer-loop step, line search, resync, series) live in
+    // LDS so that they hold no SGPRs across the loop.
+    float* cold = smem + H.cold;
+    for (int i = tid; i < kColdWords; i += P.BT) {
+        float val = 0.f;
+        if (i < IRM_MAX_LR) val = P.gd_lr[i];
+        else if (i == C_LCI) val = P.lci;
+        else if (i == C_EPSP) val = P.eps_p;
+        else if (i == C_EPSV) val = P.eps_v;
+        else if (i == C_PMAX) val = P.pmax;
+        else if (i == C_PMIN) val = P.pmin;
+        else if (i == C_VMAX) val = P.vmax;
+        else if (i == C_BLR0) val = P.bls_lr0;
+        else if (i == C_BA) val = P.bls_a;
+        else if (i == C_BP) val = P.bls_bp;
+        else if (i == C_BM) val = P.bls_bm;
+        else if (i == C_MAXOUT) val = __int_as_float(P.max_outer);
+        else if (i == C_MAXBLS) val = __int_as_float(P.max_bls);
+        else if (i == C_MAXSER) val = __int_as_float(P.max_series);
+        else if (i >= C_PTR && i < C_PTR + 8) {
+            const int w = i - C_PTR;
+            const void* ptrs[4] = {P.series, P.Vr, P.Kt, P.dKt};
+            const uint64_t a = reinterpret_cast<uint64_t>(ptrs[w >> 1]);
+            val = __uint_as_float((w & 1) ? (uint32_t)(a >> 32) : (uint32_t)a);
+        } else if (i >= C_MINV && i < C_MINV + D * D) val = P.Minv[i - C_MINV];
+        else if (i >= C_WAL && i < C_WAL + D) val = P.wal[i - C_WAL];
+        else if (i >= C_JINV && i < C_JINV + D * D) val = P.Jinv[i - C_JINV];
+        cold[i] = val;
     }
+    auto cold_ptr = [&](int w) -> float* {
+        const uint64_t lo = __float_as_uint(cold[C_PTR + 2 * w]), hi = __float_as_uint(cold[C_PTR + 2 * w + 1]);
+        return reinterpret_cast<float*>(lo | (hi << 32));
+    };
+    auto cold_int = [&](int i) { return __float_as_int(cold[i]); };
     stage_alpha<D>(P, tb0, ntb, X, NK);
     __syncthreads();
     // T0 = (K·α0)·J, V0 = (dK·α0)·J  (trajectory.py:63-65), correctly rounded.
-    // ab: this lane's row of the α the state is currently expressed against
-    // (α = cprod·ab − (V_R·yacc)·Jᵀ); α0 now, the materialised α after a resync.
-    float q[D], v[D], s[D], g[D], ydir[D], yacc[D], ab[D];
+    // ab: this lane's row of the α the state is expressed against (α0, then the α
+    // materialised at the last resync).
+    float q[D], v[D], s[D], g[D], ab[D], dT[D], dV[D], dra[D], drb[D], aca[D], acb[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) {
         q[k] = v[k] = 0.f;
-        ydir[k] = yacc[k] = 0.f;
+        dT[k] = dV[k] = dra[k] = drb[k] = aca[k] = acb[k] = 0.f;
         ab[k] = valid ? X[n * kLd + t * D + k] : 0.f;
         s[k] = tvalid ? P.start[b * D + k] : 0.f;
         g[k] = tvalid ? P.goal[b * D + k] : 0.f;
@@ -708,6 +760,60 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
     for (int e = tid; e < MP * kLd; e += P.BT) X[e] = 0.f;
     const float* obs = obsL + (P.obs_stride ? t * obs_pitch(P.O) : 0);
 
+    // stage 1 over the units of this wave: Ypart[s] = Fᵀ·[a'; b'] (velocity half if `full`)
+    auto stage1 = [&](bool full) {
+        const float* xl = X + (lane >> 4) * kLd + (lane & 15);
+        auto quads = [&](const f32x4* ap, int qoff, int k0, int k1, f32x4& acc0, f32x4& acc1) {
+            for (int kq = k0; kq < k1; ++kq) {
+                const f32x4 a = ap[(size_t)kq * 64];
+                const float* xb = xl + (qoff + kq) * 16 * kLd;
+                const float b0 = xb[0], b1 = xb[4 * kLd], b2 = xb[8 * kLd], b3 = xb[12 * kLd];
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b0, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b1, acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b2, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b3, acc1, 0, 0, 0);
+            }
+        };
+        if (REGOPS) {  // one unit per wave (regops_fit), position-half fragments in VGPRs
+            if (has1) {
+                float bv[S1Q][4];
+#pragma unroll
+                for (int i = 0; i < S1Q; ++i) {
+                    const float* xb = xl + (kq0 + i) * 16 * kLd;
+                    const bool in = kq0 + i < kq1;
+                    bv[i][0] = in ? xb[0] : 0.f;
+                    bv[i][1] = in ? xb[4 * kLd] : 0.f;
+                    bv[i][2] = in ? xb[8 * kLd] : 0.f;
+                    bv[i][3] = in ? xb[12 * kLd] : 0.f;
+                }
+                f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int i = 0; i < S1Q; ++i) {
+                    if (kq0 + i < kq1) {
+                        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][0], bv[i][0], acc0, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][1], bv[i][1], acc1, 0, 0, 0);
+                        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][2], bv[i][2], acc0, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][3], bv[i][3], acc1, 0, 0, 0);
+                    }
+                }
+                if (full)
+                    quads(reinterpret_cast<const f32x4*>(F1) + ((size_t)tile1 * KQ1 + KQa) * 64 + lane, KQa, kq0,
+                          kq1, acc0, acc1);
+                store_tile(Ypart + sp1 * RP * kLd, tile1, acc0 + acc1, 0xFFFFu, RP);
+            }
+        } else {
+            for (int u = wave; u < MT1 * nsplit; u += nwaves) {
+                const int tile = u % MT1, sp = u / MT1;
+                const int k0 = (KQa * sp) / nsplit, k1 = (KQa * (sp + 1)) / nsplit;
+                f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+                const f32x4* ap = reinterpret_cast<const f32x4*>(F1) + ((size_t)tile * KQ1) * 64 + lane;
+                quads(ap, 0, k0, k1, acc0, acc1);
+                if (full) quads(ap + (size_t)KQa * 64, KQa, k0, k1, acc0, acc1);
+                store_tile(Ypart + sp * RP * kLd, tile, acc0 + acc1, 0xFFFFu, RP);
+            }
+        }
+    };
+
     // replicated per-trajectory scalar state
     float loss = 0.f, lsg = P.lsg0, ljl = P.ljl0, lr = 0.f, cprod = 1.f, gnorm = 1.f, anorm = 0.f;
     float cfac = 1.f, step = 0.f;
@@ -721,63 +827,56 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
     IRM_STAMP(14);
 
     for (int round = 0;; ++round) {
-        // ------------------------------------------------ direction (stage 1+2)
-        const unsigned dirmask = flagw[round & 1];
+        const int par = round & 1;
+        const unsigned dirmask = flagw[par];
+        const unsigned rmask = flagw[3 + par];
+        const bool dense = flagw[5 + par] != 0u;  // b' has rows beyond the endpoints: full stage 1
         IRM_STAMP(4);
+        if (tid == 0) {  // next round's masks (set in this round's flag section)
+            flagw[par ^ 1] = 0u;
+            flagw[3 + (par ^ 1)] = 0u;
+            flagw[5 + (par ^ 1)] = 0u;
+        }
+        // ------------------------------------------------ direction (stage 1+2)
         if (dirmask) {
-            // stage 1: Ypart[s] = F_topᵀ(RP × NK) · a   (split-K over the waves)
-            if (REGOPS) {
-                if (has1) {
-                    const float* xl = X + (lane >> 4) * kLd + (lane & 15);
-                    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+            // the direction's gradient inputs: this lane's rows (α recovery) and the two
+            // endpoint velocity rows of its trajectory (sparse stage 1)
+            float e0[D], e1[D];
+            if (needs_dir) {
 #pragma unroll
-                    for (int i = 0; i < S1Q; ++i) {
-                        if (kq0 + i < kq1) {
-                            const float* xb = xl + (kq0 + i) * 16 * kLd;
-                            const float b0 = xb[0], b1 = xb[4 * kLd], b2 = xb[8 * kLd], b3 = xb[12 * kLd];
-                            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][0], b0, acc0, 0, 0, 0);
-                            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][1], b1, acc1, 0, 0, 0);
-                            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][2], b2, acc0, 0, 0, 0);
-                            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][3], b3, acc1, 0, 0, 0);
-                        }
-                    }
-                    store_tile(Ypart + sp1 * RP * kLd, tile1, acc0 + acc1, 0xFFFFu, RP);
-                }
-            } else {
-                for (int u = wave; u < MT1 * nsplit; u += nwaves) {
-                    const int tile = u % MT1, sp = u / MT1;
-                    const int k0 = (KQ1 * sp) / nsplit, k1 = (KQ1 * (sp + 1)) / nsplit;
-                    f32x4 acc = mma_tile(F1, KQ1, tile, k0, k1, X);
-                    store_tile(Ypart + sp * RP * kLd, tile, acc, 0xFFFFu, RP);
+                for (int k = 0; k < D; ++k) {
+                    dra[k] = valid ? X[n * kLd + t * D + k] : 0.f;
+                    drb[k] = valid ? X[(NK + n) * kLd + t * D + k] : 0.f;
+                    e0[k] = X[NK * kLd + t * D + k];
+                    e1[k] = X[(NK + N - 1) * kLd + t * D + k];
                 }
             }
-            if (tid == 0) flagw[(round + 1) & 1] = 0u;  // next round's direction mask
+            stage1(dense);
             IRM_STAMP(5);
             __syncthreads();
             IRM_STAMP(0);
-            // y = Σ partials; y·JᵀJ; BLS norms.  Lane n = row r of y.
-            float g2 = 0.f, al = 0.f;
-            if (yrow && needs_dir) {
-                float y[D];
+            // BLS norms from y' rows (lane n = row r):
+            //   ‖G‖² = Σ_r y'(JᵀJ)⁻¹y'ᵀ,  alpha_norm·‖G‖ = Σ_r (y'·w)², w = (JᵀJ)⁻¹Jᵀ1
+            if (bls && needs_dir) {
+                float g2 = 0.f, al = 0.f;
+                if (yrow) {
+                    float y[D];
 #pragma unroll
-                for (int d = 0; d < D; ++d) y[d] = 0.f;
-                for (int sp = 0; sp < nsplit; ++sp) {
+                    for (int d = 0; d < D; ++d) y[d] = dense ? 0.f : fmaf(fb0, e0[d], fb1 * e1[d]);
+                    for (int sp = 0; sp < nsplit; ++sp) {
 #pragma unroll
-                    for (int d = 0; d < D; ++d) y[d] += Ypart[(sp * RP + n) * kLd + t * D + d];
+                        for (int d = 0; d < D; ++d) y[d] += Ypart[(sp * RP + n) * kLd + t * D + d];
+                    }
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        float m = 0.f;
+#pragma unroll
+                        for (int d = 0; d < D; ++d) m += y[d] * cold[C_MINV + d * D + k];
+                        g2 += y[k] * m;
+                        al += cold[C_WAL + k] * y[k];
+                    }
+                    al = al * al;
                 }
-#pragma unroll
-                for (int k = 0; k < D; ++k) {
-                    float m = 0.f;
-#pragma unroll
-                    for (int d = 0; d < D; ++d) m += y[d] * P.JtJ[d * D + k];
-                    Ymix[n * kLd + t * D + k] = m;
-                    g2 += y[k] * m;        // yᵀ(JᵀJ)y  → ‖G‖²_F
-                    al += P.Jcol[k] * y[k];
-                    ydir[k] = y[k];
-                }
-                al = al * al;              // (uᵀy)²    → Σ_ij (GᵀG)_ij
-            }
-            if (bls && needs_dir) {  // optimizer_BLS.py:165-166 from W = Σ_r y_r y_rᵀ
                 g2 = wred_sum(g2);
                 al = wred_sum(al);
                 if (lane == 0) {
@@ -785,39 +884,77 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                     wp[wave * 2 + 1] = al;
                 }
             }
-            __syncthreads();
             IRM_STAMP(2);
-            // stage 2: dP = F(MP × RP) · Ymix, only the direction columns
-            if (REGOPS) {
-                const float* xl = Ymix + (lane >> 4) * kLd + (lane & 15);
-                f32x4 acc[S2T];
+            // stage 2: dP = F(MP × RP)·Σ_s Ypart[s], only the direction columns
+            {
+                const float* xl = Ypart + (lane >> 4) * kLd + (lane & 15);
+                auto bload = [&](int i, float& b0, float& b1, float& b2, float& b3) {
+                    b0 = b1 = b2 = b3 = 0.f;
+                    for (int sp = 0; sp < nsplit; ++sp) {
+                        const float* xb = xl + (sp * RP + i * 16) * kLd;
+                        b0 += xb[0];
+                        b1 += xb[4 * kLd];
+                        b2 += xb[8 * kLd];
+                        b3 += xb[12 * kLd];
+                    }
+                };
+                if (REGOPS) {
+                    f32x4 acc[S2T];
 #pragma unroll
-                for (int j = 0; j < S2T; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    for (int j = 0; j < S2T; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    float bv[2][4];
 #pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    if (i < KQ2) {
-                        const float* xb = xl + i * 16 * kLd;
-                        const float b0 = xb[0], b1 = xb[4 * kLd], b2 = xb[8 * kLd], b3 = xb[12 * kLd];
+                    for (int i = 0; i < 2; ++i) {
+                        if (i < KQ2) bload(i, bv[i][0], bv[i][1], bv[i][2], bv[i][3]);
+                    }
 #pragma unroll
-                        for (int j = 0; j < S2T; ++j) {
-                            if (wave + j * nwaves < MT2) {
-                                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][0], b0, acc[j], 0, 0, 0);
-                                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][1], b1, acc[j], 0, 0, 0);
-                                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][2], b2, acc[j], 0, 0, 0);
-                                acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][3], b3, acc[j], 0, 0, 0);
+                    for (int i = 0; i < 2; ++i) {
+                        if (i < KQ2) {
+#pragma unroll
+                            for (int j = 0; j < S2T; ++j) {
+                                if (wave + j * nwaves < MT2) {
+                                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][0], bv[i][0], acc[j], 0, 0, 0);
+                                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][1], bv[i][1], acc[j], 0, 0, 0);
+                                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][2], bv[i][2], acc[j], 0, 0, 0);
+                                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][3], bv[i][3], acc[j], 0, 0, 0);
+                                }
                             }
                         }
                     }
-                }
 #pragma unroll
-                for (int j = 0; j < S2T; ++j)
-                    if (wave + j * nwaves < MT2) store_tile(dP, wave + j * nwaves, acc[j], dirmask, MP);
-            } else {
-                mma_rows(F2, MT2, KQ2, Ymix, dP, dirmask, MP, wave, nwaves);
+                    for (int j = 0; j < S2T; ++j)
+                        if (wave + j * nwaves < MT2) store_tile(dP, wave + j * nwaves, acc[j], dirmask, MP);
+                } else {
+                    for (int tile = wave; tile < MT2; tile += nwaves) {
+                        f32x4 c0 = {0.f, 0.f, 0.f, 0.f};
+                        const f32x4* ap = reinterpret_cast<const f32x4*>(F2) + ((size_t)tile * KQ2) * 64 + lane;
+                        for (int i = 0; i < KQ2; ++i) {
+                            float b0, b1, b2, b3;
+                            bload(i, b0, b1, b2, b3);
+                            const f32x4 a = ap[(size_t)i * 64];
+                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b0, c0, 0, 0, 0);
+                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b1, c0, 0, 0, 0);
+                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b2, c0, 0, 0, 0);
+                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b3, c0, 0, 0, 0);
+                        }
+                        store_tile(dP, tile, c0, dirmask, MP);
+                    }
+                }
             }
             __syncthreads();
             IRM_STAMP(3);
             if (needs_dir) {
+                // latch this lane's direction rows (+ the endpoint-velocity columns)
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    float ut = dP[n * kLd + t * D + k], uv = dP[(NK + n) * kLd + t * D + k];
+                    if (!dense) {
+                        ut = fmaf(h0T, e0[k], fmaf(h1T, e1[k], ut));
+                        uv = fmaf(h0V, e0[k], fmaf(h1V, e1[k], uv));
+                    }
+                    dT[k] = ut;
+                    dV[k] = uv;
+                }
                 if (bls) {
                     float tg = 0.f, ta = 0.f;
                     for (int ww = 0; ww < WPT; ++ww) {
@@ -836,8 +973,6 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                 }
                 needs_dir = false;
             }
-        } else if (tid == 0) {
-            flagw[(round + 1) & 1] = 0u;
         }
         if (phase == PH_BLS_TRIAL) {
             cfac = 1.f - P.lreg * lr;
@@ -845,23 +980,35 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
         }
         // ------------------------------------------------------- resync
         // Trajectories whose inner loop ended last round: α = cprod·ab −
-        // (V_R·yacc)·Jᵀ in fp32 (what the reference carries), then [T; V] =
+        // V_R·(Fᵀ·acc)·J⁻¹ in fp32 (what the reference carries), then [T; V] =
         // eval_exact(α), so the constraint check below and the caller's
         // evaluate(α_out) see the same waypoints bit for bit.
-        const unsigned rmask = flagw[3 + (round & 1)];
-        if (tid == 0) flagw[3 + ((round + 1) & 1)] = 0u;
         if (rmask) {  // block-uniform
             const bool rs = tvalid && ((rmask >> t) & 1u);  // wave-uniform
+            if (rs && valid) {
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    X[n * kLd + t * D + k] = aca[k];
+                    X[(NK + n) * kLd + t * D + k] = acb[k];
+                }
+            }
+            __syncthreads();
+            stage1(true);
+            __syncthreads();
             if (rs && yrow) {
 #pragma unroll
-                for (int k = 0; k < D; ++k) Ymix[n * kLd + t * D + k] = yacc[k];
+                for (int d = 0; d < D; ++d) {
+                    float y = 0.f;
+                    for (int sp = 0; sp < nsplit; ++sp) y += Ypart[(sp * RP + n) * kLd + t * D + d];
+                    Ymix[n * kLd + t * D + d] = y;
+                }
             }
             __syncthreads();
             if (rs && valid) {
                 float z[D];
 #pragma unroll
                 for (int l = 0; l < D; ++l) z[l] = 0.f;
-                const float* vr = P.Vr + (size_t)n * RP;
+                const float* vr = cold_ptr(1) + (size_t)n * RP;
                 for (int r = 0; r < RP; ++r) {
                     const float vv = vr[r];
 #pragma unroll
@@ -871,7 +1018,7 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                 for (int k = 0; k < D; ++k) {
                     float acc = 0.f;
 #pragma unroll
-                    for (int l = 0; l < D; ++l) acc += z[l] * P.J[k * D + l];
+                    for (int l = 0; l < D; ++l) acc += z[l] * cold[C_JINV + l * D + k];
                     ab[k] = cprod * ab[k] - acc;
                     X[n * kLd + t * D + k] = ab[k];
                 }
@@ -879,26 +1026,27 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
             __syncthreads();
             if (rs) {
                 if (valid) {
-                    eval_exact<D>(P, X + t * D, n, q, v);
+                    eval_exact<D>(P, X + t * D, n, q, v, cold_ptr(2), cold_ptr(3));
                     // the last extended-vis frame shows the materialised α's trajectory
                     if (rec && st.series_len > 0) {
+                        float* ser = cold_ptr(0);
+                        const int ms = cold_int(C_MAXSER);
 #pragma unroll
-                        for (int k = 0; k < D; ++k)
-                            P.series[((b * P.max_series) + st.series_len - 1) * N * D + n * D + k] = q[k];
+                        for (int k = 0; k < D; ++k) ser[((b * ms) + st.series_len - 1) * N * D + n * D + k] = q[k];
                     }
                 }
                 cprod = 1.f;
 #pragma unroll
-                for (int k = 0; k < D; ++k) yacc[k] = 0.f;
+                for (int k = 0; k < D; ++k) aca[k] = acb[k] = 0.f;
             }
         }
         // ------------------------------------------------------- update
         float q2[D], v2[D];
-        if (valid && (phase == PH_GD_INNER || phase == PH_BLS_TRIAL)) {
+        if (phase == PH_GD_INNER || phase == PH_BLS_TRIAL) {
 #pragma unroll
             for (int k = 0; k < D; ++k) {
-                q2[k] = cfac * q[k] - step * dP[n * kLd + t * D + k];
-                v2[k] = cfac * v[k] - step * dP[(N + n) * kLd + t * D + k];
+                q2[k] = cfac * q[k] - step * dT[k];
+                v2[k] = cfac * v[k] - step * dV[k];
             }
         } else {
 #pragma unroll
@@ -914,14 +1062,8 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
         if (ev) {
             if (valid) eval_waypoint<D>(P, q2, v2, obs, w);
             IRM_STAMP(8);
-            EvalRed r;
-            r.cmax = valid ? w.cv : -INFINITY;
-            r.cidx = valid ? n : 0x7fffffff;
-            r.usum = valid ? P.one_m_lmax * (w.cv * P.invN) + ljl * ((w.jp + w.jv) * P.invN) : 0.f;
-            r.tx = valid ? w.tx : -INFINITY;
-            r.tn = valid ? w.tn : INFINITY;
-            r.va = valid ? w.va : 0.f;
-            ered_store(r, red, wave);
+            const float us = P.one_m_lmax * (w.cv * P.invN) + ljl * ((w.jp + w.jv) * P.invN);
+            ered_store(valid, w.cv, us, w.tx, w.tn, w.va, phase == PH_RESYNC, n0, red, wave);
             if (valid && (n == 0 || n == N - 1)) {  // trajectory.py:183-204 rows 0 and N−1
                 float a = 0.f, bb = 0.f;
 #pragma unroll
@@ -939,12 +1081,12 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
         IRM_STAMP(7);
         if (ev) {
             // combine the trajectory's wave partials (fixed order)
-            const float* r0 = red + (t * WPT) * 10;
+            const float* r0 = red + (t * WPT) * 8;
             float cmax = r0[0];
             int cidx = __float_as_int(r0[1]);
             float usum = r0[2], tx = r0[3], tn = r0[4], va = r0[5];
             for (int ww = 1; ww < WPT; ++ww) {
-                const float* rw = red + (t * WPT + ww) * 10;
+                const float* rw = red + (t * WPT + ww) * 8;
                 amax_step(cmax, cidx, rw[0], __float_as_int(rw[1]));
                 usum += rw[2];
                 tx = fmaxf(tx, rw[3]);
@@ -964,7 +1106,7 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                 loss = nl;
                 if (!bls) st.cost_evals++;
                 accept = 2;
-                lr = bls ? P.bls_lr0 : P.gd_lr[outer];
+                lr = bls ? cold[C_BLR0] : cold[outer];
                 needs_dir = true;
                 if (!bls) phase = PH_GD_INNER;
                 if (P.max_inner <= 0) to_end = true;
@@ -973,18 +1115,19 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
             } else if (phase == PH_RESYNC) {
                 // constraintsFulfilled(α) (trajectory.py:129-137, robot.py:90-113) on the
                 // materialised α; optimizer_GD.py:427-437 / optimizer_BLS.py:201-211
-                const bool ok = sqrtf(e_a0) < P.eps_p && sqrtf(e_a1) < P.eps_p && sqrtf(e_b0) < P.eps_v &&
-                                sqrtf(e_b1) < P.eps_v && tx <= P.pmax && tn >= P.pmin && va <= P.vmax;
+                const float eps_p = cold[C_EPSP], eps_v = cold[C_EPSV];
+                const bool ok = sqrtf(e_a0) < eps_p && sqrtf(e_a1) < eps_p && sqrtf(e_b0) < eps_v &&
+                                sqrtf(e_b1) < eps_v && tx <= cold[C_PMAX] && tn >= cold[C_PMIN] && va <= cold[C_VMAX];
                 st.outer_iterations++;
                 st.constraints_ok = ok ? 1 : 0;
                 if (ok) {
                     phase = PH_DONE;
                 } else {
                     outer++;
-                    lsg = lsg * P.lci;
-                    ljl = ljl * P.lci;
+                    lsg = lsg * cold[C_LCI];
+                    ljl = ljl * cold[C_LCI];
                     inner = 0;
-                    phase = (outer >= P.max_outer) ? PH_DONE : PH_OUTER_START;
+                    phase = (outer >= cold_int(C_MAXOUT)) ? PH_DONE : PH_OUTER_START;
                 }
             } else if (phase == PH_GD_INNER) {  // optimizer_GD.py:394-408
                 st.grad_evals++;
@@ -1003,16 +1146,16 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
             } else {  // PH_BLS_TRIAL: optimizer_BLS.py:136-150, 172-178
                 st.cost_evals++;
                 st.bls_trials++;
-                const float required = loss - P.bls_a * lr * anorm;
+                const float required = loss - cold[C_BA] * lr * anorm;
                 bool inner_end = false, rejected_all = false;
                 float improve = 0.f;
                 if (nl > required) {
-                    lr = lr * P.bls_bm;
+                    lr = lr * cold[C_BM];
                     trial++;
-                    if (trial >= P.max_bls) inner_end = rejected_all = true;  // new_loss = loss
+                    if (trial >= cold_int(C_MAXBLS)) inner_end = rejected_all = true;  // new_loss = loss
                 } else {
                     accept = 1;
-                    lr = lr * P.bls_bp;
+                    lr = lr * cold[C_BP];
                     improve = loss - nl;
                     loss = nl;
                     inner_end = true;
@@ -1036,16 +1179,26 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                 phase = PH_RESYNC;
             }
             IRM_STAMP(10);
-            // --------------------------------------------------- gradient inputs at T2
+            // ------------------------- gradient inputs at T2, mixed by JᵀJ (→ y' = y·JᵀJ)
+            bool bfar = false;
             if (valid) {
                 float a[D], bb[D];
                 grad_waypoint<D>(P, w, q2, v2, n, cidx, lsg_e, ljl_e, s, g, a, bb);
+                const bool endrow = (n == 0 || n == N - 1);
 #pragma unroll
                 for (int k = 0; k < D; ++k) {
-                    X[n * kLd + t * D + k] = a[k];
-                    Bs[n * kLd + t * D + k] = bb[k];
+                    float ma = 0.f, mb = 0.f;
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        ma += a[d] * P.JtJ[d * D + k];
+                        mb += bb[d] * P.JtJ[d * D + k];
+                    }
+                    X[n * kLd + t * D + k] = ma;
+                    X[(NK + n) * kLd + t * D + k] = mb;
+                    bfar |= (!endrow && bb[k] != 0.f);
                 }
             }
+            if (__ballot(bfar) && lane == 0) atomicOr(&flagw[5 + (par ^ 1)], 1u);
             IRM_STAMP(12);
             // --------------------------------------------------- accept
             if (accept == 1) {
@@ -1053,24 +1206,26 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                 for (int k = 0; k < D; ++k) {
                     q[k] = q2[k];
                     v[k] = v2[k];
-                    yacc[k] = cfac * yacc[k] + step * ydir[k];  // α recovery (rows r = n < RP)
+                    aca[k] = cfac * aca[k] + step * dra[k];  // α recovery: Σ steps·[a'; b']
+                    acb[k] = cfac * acb[k] + step * drb[k];
                 }
                 cprod *= cfac;
             }
             // extended-vis snapshot after every non-breaking inner iteration
             // (optimizer_GD.py:366-367, optimizer_BLS.py:106-107)
-            if (rec && snap && st.series_len < P.max_series) {
+            if (rec && snap && st.series_len < cold_int(C_MAXSER)) {
                 if (valid) {
+                    float* ser = cold_ptr(0);
+                    const int ms = cold_int(C_MAXSER);
 #pragma unroll
-                    for (int k = 0; k < D; ++k)
-                        P.series[((b * P.max_series) + st.series_len) * N * D + n * D + k] = q[k];
+                    for (int k = 0; k < D; ++k) ser[((b * ms) + st.series_len) * N * D + n * D + k] = q[k];
                 }
                 st.series_len++;
             }
             if (n == 0) {
-                if (needs_dir) atomicOr(&flagw[(round + 1) & 1], tmask << (t * D));
+                if (needs_dir) atomicOr(&flagw[par ^ 1], tmask << (t * D));
                 if (phase == PH_DONE) atomicOr(&flagw[2], 1u << t);
-                if (phase == PH_RESYNC) atomicOr(&flagw[3 + ((round + 1) & 1)], 1u << t);
+                if (phase == PH_RESYNC) atomicOr(&flagw[3 + (par ^ 1)], 1u << t);
             }
         }
         IRM_STAMP(15);
@@ -1080,24 +1235,13 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
     }
 
     // ----------------------------------------------------------- epilogue
-    // α = cprod·α0 − (V_R·y_acc)·Jᵀ ; trajectory = T ; stats
-    if (yrow) {
-#pragma unroll
-        for (int k = 0; k < D; ++k) Ymix[n * kLd + t * D + k] = yacc[k];
-    }
-    __syncthreads();
-    mma_rows(P.Vfrag, NK / 16, RP / 16, Ymix, dP, 0xFFFFu, NK, wave, nwaves);
-    __syncthreads();
+    // Every trajectory ended through PH_RESYNC: acc = 0, cprod = 1, α = ab and
+    // T = eval_exact(α) exactly.
     if (valid) {
 #pragma unroll
         for (int k = 0; k < D; ++k) {
             if (P.traj_out) P.traj_out[(b * N + n) * D + k] = q[k];
-            if (P.alpha_out) {
-                float acc = 0.f;
-#pragma unroll
-                for (int l = 0; l < D; ++l) acc += dP[n * kLd + t * D + l] * P.J[k * D + l];
-                P.alpha_out[(b * N + n) * D + k] = cprod * ab[k] - acc;
-            }
+            if (P.alpha_out) P.alpha_out[(b * N + n) * D + k] = ab[k];
         }
     }
     if (P.stats && tvalid && n == 0) P.stats[b] = st;
@@ -1299,22 +1443,45 @@ static hipError_t launch_lds(K kernel, int grid, int threads, size_t lds, hipStr
     return hipGetLastError();
 }
 
+template <class T>
+struct type_tag {
+    using type = T;
+};
+
 hipError_t launch_optimize(const KParams& p, hipStream_t s) {
     const bool stage = p.ops_in_lds != 0;
     const Plan L = plan_lds(p, stage, true);
     const size_t lds = (size_t)L.total * 4;
     const int grid = (p.B + p.TB - 1) / p.TB;
     if (grid <= 0) return hipSuccess;
-    return dispatch_d(p.D, [&](auto dc) {
-        constexpr int DD = decltype(dc)::value;
+    // launch k_optimize<Shape> with the MAXT / operator-placement / optimiser variants
+    auto run = [&](auto shape_tag) {
+        using Sh = typename decltype(shape_tag)::type;
         return dispatch_t(p.BT, [&](auto tc) {
             constexpr int TT = decltype(tc)::value;
-            if constexpr (TT <= 512) {
-                if (p.regops) return launch_lds(k_optimize<DD, TT, true, true>, grid, p.BT, lds, s, p);
-            }
-            return stage ? launch_lds(k_optimize<DD, TT, true, false>, grid, p.BT, lds, s, p)
-                         : launch_lds(k_optimize<DD, TT, false, false>, grid, p.BT, lds, s, p);
+            auto go = [&](auto bc) {
+                constexpr bool BB = decltype(bc)::value;
+                if constexpr (TT <= 512) {
+                    if (p.regops) return launch_lds(k_optimize<Sh, TT, true, true, BB>, grid, p.BT, lds, s, p);
+                }
+                return stage ? launch_lds(k_optimize<Sh, TT, true, false, BB>, grid, p.BT, lds, s, p)
+                             : launch_lds(k_optimize<Sh, TT, false, false, BB>, grid, p.BT, lds, s, p);
+            };
+            return p.optimizer == IRM_OPT_BLS ? go(std::integral_constant<bool, true>{})
+                                              : go(std::integral_constant<bool, false>{});
         });
+    };
+    // shape-specialised kernels for the common configurations (auto rank R = 32)
+    if (p.RP == 32 && p.nsplit == stage1_splits(p.NK)) {
+        if (p.D == 3 && p.N == 50) return run(type_tag<FixShape<3, 50, 32>>{});
+        if (p.D == 3 && p.N == 64) return run(type_tag<FixShape<3, 64, 32>>{});
+        if (p.D == 3 && p.N == 128) return run(type_tag<FixShape<3, 128, 32>>{});
+        if (p.D == 3 && p.N == 256) return run(type_tag<FixShape<3, 256, 32>>{});
+        if (p.D == 7 && p.N == 256) return run(type_tag<FixShape<7, 256, 32>>{});
+    }
+    return dispatch_d(p.D, [&](auto dc) {
+        constexpr int DD = decltype(dc)::value;
+        return run(type_tag<DynShape<DD>>{});
     });
 }
 

@@ -31,7 +31,7 @@ struct KParams {
     // shapes
     int32_t N, D, R, TB, B, O, obs_stride;
     int32_t NK;   // N rounded up to 16 (k extent of N-contractions)
-    int32_t MP;   // 2N rounded up to 16 (rows of [K;dK])
+    int32_t MP;   // 2·NK: rows of [K; dK] / [a; b] / [T; V], velocity half from row NK
     int32_t RP;   // R (multiple of 16)
     int32_t ops_in_lds;  // operator fragments staged into LDS
     int32_t NW;          // lanes per trajectory = N rounded up to 64 (whole waves)
@@ -51,7 +51,8 @@ struct KParams {
     float J[IRM_MAX_JOINTS * IRM_MAX_JOINTS];    // J (D×D, row-major, stride D)
     float JtJ[IRM_MAX_JOINTS * IRM_MAX_JOINTS];  // JᵀJ
     float Jinv[IRM_MAX_JOINTS * IRM_MAX_JOINTS]; // J⁻¹
-    float Jcol[IRM_MAX_JOINTS];                  // u = Jᵀ·1 (column sums): alpha_norm = (uᵀy)²-sum
+    float Minv[IRM_MAX_JOINTS * IRM_MAX_JOINTS]; // (JᵀJ)⁻¹
+    float wal[IRM_MAX_JOINTS];                   // (JᵀJ)⁻¹·Jᵀ1: alpha_norm·‖G‖ = Σ_r (y'_r·wal)²
     // operators (device, fp32)
     const float* Km;      // K, row-major                 (N × N)
     const float* dKm;     // dK, row-major                (N × N)
@@ -61,7 +62,7 @@ struct KParams {
     const float* F2frag;  // A-fragments of F             (MP × RP)
     const float* Fbot;    // F rows N..2N-1, row-major    (N × RP)
     const float* Vr;      // V_R, row-major               (N × RP)
-    const float* Vfrag;   // A-fragments of V_R           (NK × RP)
+    const float* Hend;    // F·F[NK]ᵀ, F·F[NK+N−1]ᵀ: operator columns of the endpoint velocity rows (2 × MP)
     const float* uvec;    // K⁻¹(1-c)   (N)  initTrajectory basis
     const float* wvec;    // K⁻¹c       (N)
     // batch I/O
@@ -112,15 +113,68 @@ struct Plan {
     int total;
 };
 
+__host__ __device__ constexpr int al4(int x) { return (x + 3) & ~3; }
+
+// Head of the LDS layout: every region whose size depends only on the shape
+// (MP, RP, nsplit), plus fixed-capacity per-wave / per-trajectory records, so that
+// a shape-specialised kernel sees compile-time offsets.  Obstacles follow; the
+// staged operator fragments (non-REGOPS, ops_in_lds) come last.
+constexpr int kMaxWaves = kMaxThreads / 64;
+constexpr int kMaxTraj = kCols;  // TB·D ≤ 16
+struct Head {
+    int X, dP, Ypart, Ymix, red, sg, wp, flags, cold, obs;
+};
+// LDS "cold" parameter block of k_optimize (word offsets)
+enum ColdWord : int {
+    C_GDLR = 0,  // IRM_MAX_LR words
+    C_LCI = 32, C_EPSP, C_EPSV, C_PMAX, C_PMIN, C_VMAX, C_BLR0, C_BA, C_BP, C_BM, C_MAXOUT, C_MAXBLS, C_MAXSER,
+    C_PTR = 46,     // 4 pointers × 2 words: series, Vr, Kt, dKt
+    C_MINV = 56,    // (JᵀJ)⁻¹, D×D
+    C_WAL = 120,    // D
+    C_JINV = 128,   // J⁻¹, D×D
+    kColdWords = 192
+};
+__host__ __device__ constexpr Head plan_head(int MP, int RP, int nsplit, bool optimizer) {
+    Head H{};
+    H.X = 0;
+    H.dP = H.X + al4(MP * kLd);
+    int off = H.dP + al4(MP * kLd);
+    H.Ypart = H.Ymix = 0;
+    if (optimizer) {
+        H.Ypart = off;
+        off += al4(nsplit * RP * kLd);
+        H.Ymix = off;
+        off += al4(RP * kLd);
+    }
+    H.red = off;
+    off += kMaxWaves * 8;
+    H.sg = off;
+    off += kMaxTraj * 4;
+    H.wp = off;
+    off += kMaxWaves * 2;
+    H.flags = off;
+    off += 8;
+    H.cold = 0;
+    if (optimizer) {
+        H.cold = off;
+        off += kColdWords;
+    }
+    H.obs = off;
+    return H;
+}
+
 __host__ __device__ Plan plan_lds(const KParams& p, bool ops_lds, bool optimizer);
+
+// Stage-1 split-K factor: units of 4 k-quads over the position half.
+__host__ __device__ constexpr int stage1_splits(int NK) { return (NK / 16 + 3) / 4; }
 
 // Can the operator A-fragments live in VGPRs (k_optimize<…, REGOPS=true>)?
 // Mirrors kS1Q / kS2T in irm_kernels.hip.
 inline bool regops_fit(const KParams& p) {
-    const int nw = p.BT / 64, MT1 = p.RP / 16, KQ1 = p.MP / 16, KQ2 = p.RP / 16, MT2 = p.MP / 16;
+    const int nw = p.BT / 64, MT1 = p.RP / 16, KQa = p.NK / 16, KQ2 = p.RP / 16, MT2 = p.MP / 16;
     if (p.BT > 512 || KQ2 > 2 || MT1 * p.nsplit > nw) return false;
-    const int s1q = p.BT <= 256 ? 8 : 4, s2t = p.BT <= 256 ? 8 : 4;
-    const int kq_per_unit = (KQ1 + p.nsplit - 1) / p.nsplit;
+    const int s1q = p.BT <= 256 ? 8 : 4, s2t = p.BT <= 256 ? 8 : 2;  // kS1Q / kS2T
+    const int kq_per_unit = (KQa + p.nsplit - 1) / p.nsplit;  // stage 1 keeps the position half in VGPRs
     const int tiles_per_wave = (MT2 + nw - 1) / nw;
     return kq_per_unit <= s1q && tiles_per_wave <= s2t;
 }

@@ -122,3 +122,32 @@ def exact_drift(cfg="c3", b=0, iters=(1, 2, 3, 5, 10, 20), ranks=(0, -1), lmaxs=
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "exact":
     exact_drift()
     exact_drift("c4", 0, iters=(1, 5, 20), ranks=(0,), lmaxs=(0.0,))
+
+
+def one_step(N=50, rank=0, D=3):
+    """One GD step (bench mode) vs fp64: prints the error of T and V after the step."""
+    import bench
+    from oracle.ref64 import Ref64
+    args = irm_main.parse_args(["--optimizer-name", "gd", "--n-timesteps", str(N), "--max-outer-iteration", "1",
+                                "--max-inner-iteration", "1", "--loop-loss-reduction=-1e30"])
+    p = params_from_args(args, operator_rank=rank)
+    ctx, orc = Context(p), Oracle(p)
+    _, K, dK, J = orc.kernel_matrices()
+    r = Ref64(p, K, dK, J)
+    env = Environment()
+    a0 = orc.init_alpha(env.start_config, env.goal_config)
+    alpha, traj, st = ctx.optimize(env.start_config, env.goal_config, env.obstacles, alpha0=a0)
+    a64, l64, n = r.gd_single(a0, env.obstacles, env.start_config, env.goal_config, 1)
+    T64, V64 = r.traj_vel(a64)
+    T0, V0 = r.traj_vel(a0)
+    dT = traj - T0
+    dT64 = T64 - T0
+    line(f"  N={N} rank={rank}: |T-T64| {np.abs(traj - T64).max():.3e}  |dT| {np.abs(dT).max():.3e} "
+         f"|dT64| {np.abs(dT64).max():.3e} ratio {np.sum(dT * dT64) / np.sum(dT64 * dT64):.4f} "
+         f"loss {float(st['final_loss']):.6f} vs {l64:.6f} stats {dict((k, int(v)) for k, v in st.items() if k != 'final_loss')}")
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "step":
+    for N in (50, 64, 128):
+        for rank in (0, -1):
+            one_step(N, rank)

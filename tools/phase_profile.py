@@ -16,9 +16,10 @@ import bench  # noqa: E402
 from irm_motion_planning_amd.context import Context  # noqa: E402
 from irm_motion_planning_amd.params import params_from_args  # noqa: E402
 
-PHASES = ["dir:stage1 barrier-wait", "dir:reduce+sparse", "dir:W+mix", "dir:stage2", "round-top (flags)",
-          "dir:stage1 mfma (w0)", "post-dir + update", "E1 barrier-wait", "eval_waypoint", "eval_partials",
-          "finalize+decide", "end barrier-wait", "grad_waypoint+store", "epilogue", "prologue", "accept+yacc+flags"]
+PHASES = ["dir:stage1 barrier-wait", "(unused)", "dir:y rows + BLS norms", "dir:stage2 + barrier", "round-top (flags)",
+          "dir:endpoint + stage1 mfma", "post-dir + resync + update", "E1 barrier-wait", "eval_waypoint",
+          "eval reductions", "finalize+decide", "end barrier-wait", "grad inputs (mixed) + b flag", "epilogue",
+          "prologue", "accept+yacc+flags"]
 
 
 def run(cfg, tb=0, rank=0, faithful=False):
