@@ -30,6 +30,7 @@
 namespace irm {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // ------------------------------------------------------------ LDS planning
 
@@ -148,52 +149,25 @@ struct Prof {
     __device__ __forceinline__ void flush(unsigned long long*) {}
 #endif
 };
+#ifdef IRM_ISA_MARKS  // analysis builds: phase markers in the emitted assembly
+#define IRM_STAMP(ph) asm volatile("; IRM_PHASE " #ph)
+#else
 #define IRM_STAMP(ph)                         \
     do {                                      \
         if (threadIdx.x == 0) prof.stamp(ph); \
     } while (0)
+#endif
 
 // ---------------------------------------------------------- MFMA contraction
-// acc(16×16 tile) = Σ_{kq∈[kq0,kq1)} A[tile, kq] · X[16kq .. 16kq+15][0..15]
-// A: 16x16x4 A-fragments (frag_index layout), one float4 per lane = 4 k-steps.
-// X: LDS, row stride kLd floats (one row per k); lane l reads row 4j+(l>>4),
-// column l&15 of each k-step.
-__device__ __forceinline__ f32x4 mma_tile(const float* __restrict__ A, int KQ, int tile, int kq0, int kq1,
-                                          const float* __restrict__ X) {
-    const int lane = threadIdx.x & 63;
-    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    const float* xl = X + (lane >> 4) * kLd + (lane & 15);
-    const f32x4* ap = reinterpret_cast<const f32x4*>(A) + ((size_t)tile * KQ) * 64 + lane;
-    for (int kq = kq0; kq < kq1; ++kq) {
-        f32x4 a = ap[(size_t)kq * 64];
-        const float* xb = xl + kq * 16 * kLd;
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], xb[0], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], xb[4 * kLd], acc1, 0, 0, 0);
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], xb[8 * kLd], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], xb[12 * kLd], acc1, 0, 0, 0);
-    }
-    return acc0 + acc1;
-}
-
 // D layout of 16x16x4: lane l holds rows 4*(l>>4)+i, column l&15.
-__device__ __forceinline__ void store_tile(float* out, int tile, f32x4 acc, unsigned colmask, int rows) {
+// Callers keep every tile inside the buffer (row extents are multiples of 16).
+__device__ __forceinline__ void store_tile(float* out, int tile, f32x4 acc, unsigned colmask) {
     const int lane = threadIdx.x & 63;
     const int col = lane & 15;
     if (!((colmask >> col) & 1u)) return;
+    float* o = out + (tile * 16 + 4 * (lane >> 4)) * kLd + col;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        int row = tile * 16 + 4 * (lane >> 4) + i;
-        if (row < rows) out[row * kLd + col] = acc[i];
-    }
-}
-
-// out[MT tiles] = A · X over all K; tiles dealt round-robin to the waves.
-__device__ void mma_rows(const float* A, int MT, int KQ, const float* X, float* out, unsigned colmask, int rows,
-                         int wave, int nwaves) {
-    for (int tile = wave; tile < MT; tile += nwaves) {
-        f32x4 acc = mma_tile(A, KQ, tile, 0, KQ, X);
-        store_tile(out, tile, acc, colmask, rows);
-    }
+    for (int i = 0; i < 4; ++i) o[i * kLd] = acc[i];
 }
 
 // ------------------------------------------------ per-waypoint physics
@@ -255,28 +229,30 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
         w.jx[d] = (xs[d] + Sx) - Cx;
         w.jy[d] = (ys[d] + Sy) - Cy;
     }
-    // Obstacles are staged in LDS padded to a multiple of 4 with sentinels at
-    // (1e20, 1e20): r² overflows to +inf, rcp → 0, so a sentinel adds exactly 0.
-    float cv = 0.f, ax = 0.f, ay = 0.f;
-    auto pair = [&](float ox, float oy) {
-        const float dx = fx - ox, dy = fy - oy;
-        const float r2 = dx * dx + dy * dy;
-        const float den = 0.5f + 0.5f * r2;
-        const float inv = __builtin_amdgcn_rcpf(den);
-        cv += 0.8f * inv;
-        const float i2 = inv * inv;
-        ax += (-0.8f * dx) * i2;
-        ay += (-0.8f * dy) * i2;
+    // Obstacles are staged in LDS in pairs (x_a, x_b, y_a, y_b), padded to a multiple of 4
+    // with sentinels at (1e20, 1e20): r² overflows to +inf, rcp → 0, so a sentinel adds
+    // exactly 0.  Two obstacles per packed-fp32 instruction; the even- and odd-numbered
+    // obstacles accumulate separately and are added at the end.
+    f32x2 cv2 = {0.f, 0.f}, ax2 = {0.f, 0.f}, ay2 = {0.f, 0.f};
+    const f32x2 fx2 = {fx, fx}, fy2 = {fy, fy};
+    auto pair2 = [&](f32x2 ox, f32x2 oy) {
+        const f32x2 dx = fx2 - ox, dy = fy2 - oy;
+        const f32x2 r2 = dx * dx + dy * dy;
+        const f32x2 den = 0.5f + 0.5f * r2;
+        const f32x2 inv = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+        cv2 += 0.8f * inv;
+        const f32x2 i2 = inv * inv;
+        ax2 += (-0.8f * dx) * i2;
+        ay2 += (-0.8f * dy) * i2;
     };
     const f32x4* o4 = reinterpret_cast<const f32x4*>(ob);
     const int nq = (P.O + 3) >> 2;
     for (int c = 0; c < nq; ++c) {
         const f32x4 p0 = o4[2 * c], p1 = o4[2 * c + 1];
-        pair(p0[0], p0[1]);
-        pair(p0[2], p0[3]);
-        pair(p1[0], p1[1]);
-        pair(p1[2], p1[3]);
+        pair2(p0.xy, p0.zw);
+        pair2(p1.xy, p1.zw);
     }
+    const float cv = cv2.x + cv2.y, ax = ax2.x + ax2.y, ay = ay2.x + ay2.y;
     w.cv = cv;
     w.gx = ax;
     w.gy = ay;
@@ -419,10 +395,13 @@ __device__ void stage_obstacles(const KParams& P, int tb0, int ntb, float* obsL)
     const int pitch = obs_pitch(P.O), nsets = P.obs_stride ? P.TB : 1;
     for (int e = threadIdx.x; e < nsets * pitch; e += P.BT) {
         const int tt = e / pitch, r = e - tt * pitch;
+        // r = 4·pair + 2·coord + j  →  obstacle 2·pair + j, coordinate coord
+        const int o = 2 * (r >> 2) + (r & 1), coord = (r >> 1) & 1;
         float val = 1.0e20f;
-        if (r < P.O * 2) {
-            if (!P.obs_stride) val = P.obstacles[r];
-            else if (tt < ntb) val = P.obstacles[(size_t)(tb0 + tt) * P.obs_stride + r];
+        if (o < P.O) {
+            const int src = 2 * o + coord;
+            if (!P.obs_stride) val = P.obstacles[src];
+            else if (tt < ntb) val = P.obstacles[(size_t)(tb0 + tt) * P.obs_stride + src];
         }
         obsL[e] = val;
     }
@@ -799,7 +778,7 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                 if (full)
                     quads(reinterpret_cast<const f32x4*>(F1) + ((size_t)tile1 * KQ1 + KQa) * 64 + lane, KQa, kq0,
                           kq1, acc0, acc1);
-                store_tile(Ypart + sp1 * RP * kLd, tile1, acc0 + acc1, 0xFFFFu, RP);
+                store_tile(Ypart + sp1 * RP * kLd, tile1, acc0 + acc1, 0xFFFFu);
             }
         } else {
             for (int u = wave; u < MT1 * nsplit; u += nwaves) {
@@ -809,7 +788,7 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                 const f32x4* ap = reinterpret_cast<const f32x4*>(F1) + ((size_t)tile * KQ1) * 64 + lane;
                 quads(ap, 0, k0, k1, acc0, acc1);
                 if (full) quads(ap + (size_t)KQa * 64, KQa, k0, k1, acc0, acc1);
-                store_tile(Ypart + sp * RP * kLd, tile, acc0 + acc1, 0xFFFFu, RP);
+                store_tile(Ypart + sp * RP * kLd, tile, acc0 + acc1, 0xFFFFu);
             }
         }
     };
@@ -923,7 +902,7 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                     }
 #pragma unroll
                     for (int j = 0; j < S2T; ++j)
-                        if (wave + j * nwaves < MT2) store_tile(dP, wave + j * nwaves, acc[j], dirmask, MP);
+                        if (wave + j * nwaves < MT2) store_tile(dP, wave + j * nwaves, acc[j], dirmask);
                 } else {
                     for (int tile = wave; tile < MT2; tile += nwaves) {
                         f32x4 c0 = {0.f, 0.f, 0.f, 0.f};
@@ -937,7 +916,7 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
                             c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b2, c0, 0, 0, 0);
                             c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b3, c0, 0, 0, 0);
                         }
-                        store_tile(dP, tile, c0, dirmask, MP);
+                        store_tile(dP, tile, c0, dirmask);
                     }
                 }
             }
