@@ -168,6 +168,14 @@ def load_library(path=None):
             f"{path} not found: build the HIP library first "
             "(python -c 'import __graft_entry__ as g; g.build()')"
         )
+    # One HIP runtime per process.  torch ships its own libamdhip64 (SONAME libamdhip64.so.7,
+    # but torch's libraries NEED it as "libamdhip64.so"): loaded after ours, the loader maps a
+    # second runtime and torch then finds "No HIP GPUs".  Loaded first, ours resolves to torch's
+    # copy by SONAME.  So torch, when present, is imported before the library.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     for name, (res, args) in PROTOTYPES.items():
         fn = getattr(lib, name)

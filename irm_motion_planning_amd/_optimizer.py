@@ -60,10 +60,15 @@ class _PersistentOptimizer:
         self.last_trajectory = traj
         return alpha
 
-    def optimize_batch(self, start, goal, obstacles=None, alpha0=None, obstacle_stride=0):
-        """Batched optimize(): B independent start/goal problems (B×D each)."""
+    def optimize_batch(self, start, goal, obstacles=None, alpha0=None, obstacle_stride=0, series=False):
+        """Batched optimize(): B independent start/goal problems (B×D each).
+
+        Returns (alpha, traj, stats) — plus the B × S × N × D snapshot buffer with
+        series=True (stats["series_len"] frames valid per problem)."""
         obstacles = self.env.obstacles if obstacles is None else obstacles
-        alpha, traj, stats = self.context.optimize(start, goal, obstacles, alpha0=alpha0,
-                                                   obstacle_stride=obstacle_stride)
-        self.last_stats = stats
-        return alpha, traj, stats
+        start = np.asarray(start, np.float32).reshape(-1, self.trajectory.robot.N_joints)
+        goal = np.asarray(goal, np.float32).reshape(-1, self.trajectory.robot.N_joints)
+        res = self.context.optimize(start, goal, obstacles, alpha0=alpha0, obstacle_stride=obstacle_stride,
+                                    series=series)
+        self.last_stats = res[2]
+        return res

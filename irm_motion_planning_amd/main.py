@@ -14,6 +14,7 @@ import time
 
 import numpy as np
 
+from . import batch_io
 from .optimizer_BLS import BacktrackingLineSearchOptimizer
 from .optimizer_GD import GradientDescentOptimizer
 
@@ -98,7 +99,8 @@ def build_parser():
                         help="Minimum allowable position for the robot's joints (default: -1)")
     # Additive (this build)
     parser.add_argument('--batch-size', type=int, default=1,
-                        help="Optimise this many problems at once (>1: random start/goal around the defaults)")
+                        help="Optimise this many problems in one launch (>1: problem 0 is the reference "
+                             "environment, the rest random start/goal; writes the batch files of batch_io.py)")
     parser.add_argument('--seed', type=int, default=1, help="Seed of the random batch problems (default: 1)")
     parser.add_argument('--operator-rank', type=int, default=0,
                         help="Kernel-operator rank inside the loop: 0 auto, -1 dense exact (default: 0)")
@@ -110,6 +112,47 @@ def parse_args(argv=None):
     return build_parser().parse_args(argv)
 
 
+def run_batch(optimizer, args):
+    """--batch-size B > 1: B problems in one launch per optimize().
+
+    Timing lines as main.py:118-128 (one "took" per measurement, for the whole batch); the
+    reference's report and files for problem 0 (the reference environment); batch files
+    and a one-line batch summary (batch_io.py)."""
+    env, tr = optimizer.env, optimizer.trajectory
+    start, goal = batch_io.batch_problems(args.batch_size, tr.robot.N_joints, args.seed)
+    runtimes = []
+    res = None
+    for _ in range(args.n_measurements):
+        st = time.time()
+        for _ in range(args.n_times):
+            res = optimizer.optimize_batch(start, goal, env.obstacles, series=args.extended_vis)
+        et = time.time()
+        runtimes.append(1000 * (et - st) / args.n_times)
+        print("took", 1000 * (et - st) / args.n_times, "ms")
+    if args.n_measurements > 1:
+        print("runtimes in ms: mean", np.mean(runtimes), "stddev", np.std(runtimes))
+    alpha, traj, stats = res[:3]
+    avg = tr.compute_trajectory_cost(alpha, env.obstacles, start, goal, 0, 0, 0)
+    mx = tr.compute_trajectory_cost(alpha, env.obstacles, start, goal, 0, 0, 1)
+    ok, _ = optimizer.context.constraints(alpha, start, goal)
+    print("batch of", len(alpha), "problems: constraint fulfiled", int(np.sum(ok)), "of", len(alpha),
+          "; avg cost mean", float(np.mean(avg)), ", max cost mean", float(np.mean(mx)),
+          "; inner iterations", int(np.sum(stats["inner_iterations"])))
+    ok0 = tr.constraintsFulfilledVerbose(alpha[0], start[0], goal[0], verbose=True)
+    print("result cost: ( avg", avg[0], ", max", mx[0], "). constraint fulfiled", ok0)
+    batch_io.write_result(batch_io.RESULT, traj[0])
+    batch_io.write_result_batch(batch_io.RESULT_BATCH, traj)
+    batch_io.write_summary(batch_io.SUMMARY_BATCH, avg, mx, ok, stats)
+    if args.extended_vis:
+        series = res[3]
+        lens = stats["series_len"]
+        frames0 = series[0][: int(lens[0])]
+        print(frames0.shape)
+        batch_io.write_series(batch_io.SERIES, frames0, tr.N_timesteps, tr.robot.N_joints)
+        batch_io.write_series_batch(batch_io.SERIES_BATCH, series, lens)
+    return alpha
+
+
 def main(argv=None):
     args = parse_args(argv)
     if args.optimizer_name == 'bls':
@@ -119,6 +162,8 @@ def main(argv=None):
     else:  # unreachable (argparse choices); kept for parity with main.py:113-115
         print("FATAL: not defined optimizer", args.optimizer_name)
         raise SystemExit(-1)
+    if args.batch_size > 1:
+        return run_batch(optimizer, args)
 
     def multiple_optimizations():
         runtimes = []

@@ -1,0 +1,141 @@
+"""SURVEY.md §8f rows on the GPU: batched CLI + output files (row 2) and dynamic
+environments with warm-started re-planning (row 4), against the CPU oracle.
+
+Tolerances: a few GD steps from the same α0 agree with the oracle's fp32 α-space
+iteration within 2e-3 in waypoint space (smoke() / test_gd_steps use the same band);
+HIP-vs-HIP comparisons of the same launch configuration are bit-exact.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOAL, START, obstacles, oracle_for, ref_args
+
+pytestmark = pytest.mark.gpu
+
+GD20 = ("--optimizer-name", "gd", "--max-outer-iteration", "1", "--max-inner-iteration", "20",
+        "--loop-loss-reduction=-1e30")
+
+
+def _oracle_traj(orc, alpha0, obs, s, g):
+    a, st = orc.optimize(alpha0, obs, s, g)
+    return orc.evaluate(a), st
+
+
+def test_main_cli_batch_mode(tmp_path, capsys):
+    """--batch-size B: problem 0 keeps the reference files, the batch files hold every problem,
+    each problem's trajectory matches the oracle run of the same start/goal."""
+    from irm_motion_planning_amd import batch_io
+    from irm_motion_planning_amd import main as irm_main
+    B = 12
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        irm_main.main(list(GD20) + ["--batch-size", str(B), "--seed", "3", "--extended-vis", "true",
+                                    "--n-measurements", "2"])
+    finally:
+        os.chdir(cwd)
+    out = capsys.readouterr().out
+    assert "batch of 12 problems" in out and "result cost: ( avg" in out and "runtimes in ms: mean" in out
+    res0 = np.loadtxt(tmp_path / batch_io.RESULT)
+    allr = batch_io.read_result_batch(tmp_path / batch_io.RESULT_BATCH, 50, 3)
+    assert res0.shape == (50, 3) and allr.shape == (B, 50, 3)
+    np.testing.assert_array_equal(res0, allr[0])
+    ser0 = np.loadtxt(tmp_path / batch_io.SERIES)
+    frames = batch_io.read_series_batch(tmp_path / batch_io.SERIES_BATCH)
+    assert len(frames) == B and ser0.shape == (21, 150)  # frame 0 + 20 accepted steps
+    np.testing.assert_array_equal(ser0.reshape(-1, 50, 3).astype(np.float32), frames[0])
+    for b in range(B):
+        np.testing.assert_array_equal(frames[b][-1], allr[b].astype(np.float32))
+    summ = np.loadtxt(tmp_path / batch_io.SUMMARY_BATCH)
+    assert summ.shape == (B, 6) and np.all(summ[:, 5] == 20)
+    s, g = batch_io.batch_problems(B, 3, 3)
+    orc = oracle_for(*GD20)
+    for b in (0, 5, B - 1):
+        t_o, st_o = _oracle_traj(orc, orc.init_alpha(s[b], g[b]), obstacles(), s[b], g[b])
+        assert np.abs(allr[b] - t_o).max() < 2e-3, b
+        assert abs(summ[b, 0] - orc.cost(orc.optimize(orc.init_alpha(s[b], g[b]), obstacles(), s[b], g[b])[0],
+                                          obstacles(), s[b], g[b], 0, 0, 0)) < 1e-3
+
+
+def _moved(obs, k):
+    """The reference obstacles drifting by k·(0.05, −0.03)."""
+    return (obs + np.float32(k) * np.array([0.05, -0.03], np.float32)).astype(np.float32)
+
+
+def test_replanner_cold_and_warm_equal_host_entry_point():
+    """Cold plan == irm_optimize_batch; warm plan == irm_optimize_batch(alpha0 = previous α)."""
+    from irm_motion_planning_amd.context import Context
+    from irm_motion_planning_amd.params import params_from_args
+    from irm_motion_planning_amd.replanning import Replanner
+    args = ref_args(*GD20)
+    B = 40
+    rng = np.random.default_rng(21)
+    s = rng.uniform(-0.5, 0.5, (B, 3)).astype(np.float32)
+    g = rng.uniform(0.2, 1.6, (B, 3)).astype(np.float32)
+    rp = Replanner(args, batch=B, n_obstacles=11)
+    c = Context(params_from_args(args))
+    obs0 = obstacles()
+    st0 = rp.plan(obs0, s, g)
+    a_h, t_h, st_h = c.optimize(s, g, obs0)
+    np.testing.assert_array_equal(rp.alpha_host(), a_h)
+    np.testing.assert_array_equal(rp.trajectory_host(), t_h)
+    np.testing.assert_array_equal(st0["grad_evals"], st_h["grad_evals"])
+    prev = a_h
+    for k in (1, 2, 3):
+        obs_k = _moved(obs0, k)
+        rp.plan(obs_k)  # warm start, start/goal kept
+        a_w, t_w, _ = c.optimize(s, g, obs_k, alpha0=prev)
+        np.testing.assert_array_equal(rp.alpha_host(), a_w)
+        np.testing.assert_array_equal(rp.trajectory_host(), t_w)
+        prev = a_w
+    # warm_start=False is the cold plan of the current environment
+    rp.plan(obs0, warm_start=False)
+    np.testing.assert_array_equal(rp.trajectory_host(), t_h)
+
+
+def test_replanner_warm_start_matches_oracle():
+    """A warm-started plan is the reference iteration started from the previous α."""
+    from irm_motion_planning_amd.replanning import Replanner
+    args = ref_args(*GD20)
+    B = 6
+    rng = np.random.default_rng(5)
+    s = rng.uniform(-0.5, 0.5, (B, 3)).astype(np.float32)
+    g = rng.uniform(0.2, 1.6, (B, 3)).astype(np.float32)
+    rp = Replanner(args, batch=B, n_obstacles=11)
+    orc = oracle_for(*GD20)
+    obs0 = obstacles()
+    rp.plan(obs0, s, g)
+    prev = rp.alpha_host()
+    obs1 = _moved(obs0, 4)
+    st = rp.plan(obs1)
+    traj = rp.trajectory_host()
+    for b in range(B):
+        t_o, st_o = _oracle_traj(orc, prev[b], obs1, s[b], g[b])
+        assert np.abs(traj[b] - t_o).max() < 2e-3, b
+        assert int(st["grad_evals"][b]) == st_o["grad_evals"] == 20
+
+
+def test_replanner_per_problem_obstacles():
+    """Each problem its own (moving) obstacle set: equals the shared-environment run of that
+    problem alone (batch independence, summation-tile tolerance as test_batch_equals_single)."""
+    from irm_motion_planning_amd.context import Context
+    from irm_motion_planning_amd.params import params_from_args
+    from irm_motion_planning_amd.replanning import Replanner
+    args = ref_args(*GD20)
+    B, O = 5, 7
+    rng = np.random.default_rng(8)
+    s = rng.uniform(-0.5, 0.5, (B, 3)).astype(np.float32)
+    g = rng.uniform(0.2, 1.6, (B, 3)).astype(np.float32)
+    obs = rng.uniform(-3, 3, (B, O, 2)).astype(np.float32)
+    rp = Replanner(args, batch=B, n_obstacles=O, per_problem_obstacles=True)
+    rp.plan(obs, s, g)
+    c = Context(params_from_args(args))
+    prev = rp.alpha_host()
+    obs2 = (obs + 0.1).astype(np.float32)
+    rp.plan(obs2)
+    traj = rp.trajectory_host()
+    for b in range(B):
+        _, t1, _ = c.optimize(s[b], g[b], obs2[b], alpha0=prev[b])
+        np.testing.assert_allclose(traj[b], t1, rtol=0, atol=1e-4)
