@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define IRM_ABI_VERSION 1
+#define IRM_ABI_VERSION 2
 
 #define IRM_MAX_JOINTS 8       /* D  */
 #define IRM_MAX_TIMESTEPS 256  /* N  */
@@ -97,6 +97,11 @@ typedef struct irm_params {
     int32_t record_series;  /* keep per-iteration snapshots (--extended-vis) */
     int32_t max_series;     /* snapshot capacity per trajectory (0 = auto) */
     int32_t traj_per_block; /* trajectories per workgroup (0 = auto)       */
+    /* --- additive cost variant (ABI 2) --- */
+    int32_t whole_robot_cost; /* 0: end-effector obstacle cost (the reference's,
+                                 trajectory.py:113-126); 1: summed over every
+                                 joint position fk_j, j = 1..D (robot.py:39-72;
+                                 DevBlog-Theme/blog-post.html:491-498)       */
 } irm_params;
 
 /* Per-trajectory statistics of one optimize() call. */
@@ -192,6 +197,11 @@ int irm_constraints(irm_ctx* ctx, const float* alpha, const float* start, const 
 /* Robot.fk + Robot.jacobian — robot.py:29-36, 75-87: pos_out B×2×N,
  * jac_out B×2×N×D (nullable). */
 int irm_fk(irm_ctx* ctx, const float* traj, int32_t batch, float* pos_out, float* jac_out);
+
+/* Robot.fk_joint_1..3 — robot.py:39-72 (generalised to j = 1..D): position of
+ * joint j (FK of the first j links) for every waypoint, pos_out B×D×2×N
+ * (pos_out[b][j-1] = fk_joint_j(traj[b]); fk_joint_D = fk).  ABI 2. */
+int irm_fk_joints(irm_ctx* ctx, const float* traj, int32_t batch, float* pos_out);
 
 /* environment.compute_cost_vg — environment.py:46-58 (cost_g nullable ⇒
  * compute_cost, environment.py:32-43): f B×2×N → cost_v B×N, cost_g B×2×N. */

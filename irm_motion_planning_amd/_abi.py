@@ -11,7 +11,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("IRM_LIB") or os.path.join(HERE, "libirm_hip.so")
 
-IRM_ABI_VERSION = 1
+IRM_ABI_VERSION = 2
 IRM_MAX_JOINTS = 8
 IRM_MAX_TIMESTEPS = 256
 IRM_MAX_OBSTACLES = 64
@@ -65,6 +65,7 @@ class IrmParams(ctypes.Structure):
         ("record_series", ctypes.c_int32),
         ("max_series", ctypes.c_int32),
         ("traj_per_block", ctypes.c_int32),
+        ("whole_robot_cost", ctypes.c_int32),
     ]
 
 
@@ -141,6 +142,7 @@ PROTOTYPES = {
         ctypes.c_int, [ctypes.c_void_p, c_float_p, c_float_p, c_float_p, ctypes.c_int32, c_uint8_p, c_float_p]
     ),
     "irm_fk": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_int32, c_float_p, c_float_p]),
+    "irm_fk_joints": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_int32, c_float_p]),
     "irm_compute_cost_vg": (
         ctypes.c_int, [ctypes.c_void_p, c_float_p, c_float_p, ctypes.c_int32, ctypes.c_int32, c_float_p, c_float_p]
     ),

@@ -159,6 +159,14 @@ class Context:
             jac = None if jac is None else jac[0]
         return (pos, jac) if with_jacobian else pos
 
+    def fk_joints(self, traj):
+        """Positions of every joint, B×D×2×N (robot.py:39-72 fk_joint_j for j = 1..D)."""
+        q, single = self._batch(traj, (self.N, self.D))
+        B = q.shape[0]
+        pos = np.zeros((B, self.D, 2, self.N), np.float32)
+        check(self.lib.irm_fk_joints(self._h, _ptr(q), B, _ptr(pos)))
+        return pos[0] if single else pos
+
     def compute_cost_vg(self, f, obstacles, with_grad=True):
         x, single = self._batch(f, (2, self.N))
         B = x.shape[0]

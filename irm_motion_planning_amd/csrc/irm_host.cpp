@@ -631,6 +631,7 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
     kp.lam_max = p->lambda_max_cost;
     kp.one_m_lmax = (float)(1.0 - (double)p->lambda_max_cost);
     kp.record_series = p->record_series ? 1 : 0;
+    kp.whole_robot = p->whole_robot_cost ? 1 : 0;
     c->max_series = p->max_series > 0 ? p->max_series : 1 + p->max_outer_iteration * p->max_inner_iteration;
     kp.max_series = c->max_series;
 
@@ -820,6 +821,25 @@ int irm_fk(irm_ctx* c, const float* traj, int32_t B, float* pos_out, float* jac_
                            c->stream));
     HIP_TRY(hipMemcpyAsync(pos_out, d + o_p, (size_t)B * 2 * N * 4, hipMemcpyDeviceToHost, c->stream));
     if (jac_out) HIP_TRY(hipMemcpyAsync(jac_out, d + o_j, 2 * nd * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return IRM_OK;
+}
+
+int irm_fk_joints(irm_ctx* c, const float* traj, int32_t B, float* pos_out) {
+    if (!c || !traj || !pos_out) return fail(IRM_EINVAL, "irm_fk_joints: null argument");
+    if (set_device(c)) return IRM_EDEVICE;
+    if (B <= 0) return B == 0 ? IRM_OK : fail(IRM_EINVAL, "negative batch");
+    const int N = c->N, D = c->D;
+    const size_t nd = (size_t)B * N * D;
+    Stage st{c};
+    const size_t o_q = st.take(nd * 4), o_p = st.take(2 * nd * 4);
+    if (ensure_io(c, st.off)) return IRM_ENOMEM;
+    char* d = st.base();
+    KParams kp = c->kp;
+    kp.B = B;
+    HIP_TRY(hipMemcpyAsync(d + o_q, traj, nd * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(irm::launch_fk_joints(kp, (const float*)(d + o_q), (float*)(d + o_p), c->stream));
+    HIP_TRY(hipMemcpyAsync(pos_out, d + o_p, 2 * nd * 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return IRM_OK;
 }

@@ -204,11 +204,16 @@ struct WP {
 
 // robot.py:29-36 (fk), 75-87 (jacobian); environment.py:46-58
 // (compute_cost_vg); trajectory.py:215-227, 245-255 (penalty elements).
-template <int D>
+// WHOLE: the potential is summed over every joint position p_j = fk_joint_j
+// (robot.py:39-72; DevBlog-Theme/blog-post.html:491-498) instead of the end
+// effector only.  Its gradient w.r.t. angle k is Σ_{l≥k} (X_l·GX_l + Y_l·GY_l)
+// with (X_l, Y_l) = L_l·(−sin c_l, cos c_l) and GX_l = Σ_{j≥l} ∂cost/∂p_j; it is
+// returned as w.jx (with w.gx = 1, w.jy = w.gy = 0) so grad_waypoint is shared.
+template <int D, bool WHOLE = false>
 __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)[D], const float (&v)[D],
                                               const float* __restrict__ ob, WP<D>& w) {
     float cum = 0.f, fx = 0.f, fy = 0.f, Sx = 0.f, Sy = 0.f;
-    float xs[D], ys[D];
+    float xs[D], ys[D], px[D], py[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         cum += q[d];
@@ -216,46 +221,72 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
         sincos_fast(cum, sn, cs);
         fx += P.link[d] * cs;
         fy += P.link[d] * sn;
+        px[d] = fx;
+        py[d] = fy;
         xs[d] = -(P.link[d] * sn);
         ys[d] = P.link[d] * cs;
         Sx += xs[d];
         Sy += ys[d];
     }
-    float Cx = 0.f, Cy = 0.f;
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-        Cx += xs[d];
-        Cy += ys[d];
-        w.jx[d] = (xs[d] + Sx) - Cx;
-        w.jy[d] = (ys[d] + Sy) - Cy;
-    }
     // Obstacles are staged in LDS in pairs (x_a, x_b, y_a, y_b), padded to a multiple of 4
     // with sentinels at (1e20, 1e20): r² overflows to +inf, rcp → 0, so a sentinel adds
     // exactly 0.  Two obstacles per packed-fp32 instruction; the even- and odd-numbered
     // obstacles accumulate separately and are added at the end.
-    f32x2 cv2 = {0.f, 0.f}, ax2 = {0.f, 0.f}, ay2 = {0.f, 0.f};
-    const f32x2 fx2 = {fx, fx}, fy2 = {fy, fy};
-    auto pair2 = [&](f32x2 ox, f32x2 oy) {
-        const f32x2 dx = fx2 - ox, dy = fy2 - oy;
-        const f32x2 r2 = dx * dx + dy * dy;
-        const f32x2 den = 0.5f + 0.5f * r2;
-        const f32x2 inv = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
-        cv2 += 0.8f * inv;
-        const f32x2 i2 = inv * inv;
-        ax2 += (-0.8f * dx) * i2;
-        ay2 += (-0.8f * dy) * i2;
-    };
     const f32x4* o4 = reinterpret_cast<const f32x4*>(ob);
     const int nq = (P.O + 3) >> 2;
-    for (int c = 0; c < nq; ++c) {
-        const f32x4 p0 = o4[2 * c], p1 = o4[2 * c + 1];
-        pair2(p0.xy, p0.zw);
-        pair2(p1.xy, p1.zw);
+    auto potential = [&](float x, float y, float& cv, float& ax, float& ay) {
+        f32x2 cv2 = {0.f, 0.f}, ax2 = {0.f, 0.f}, ay2 = {0.f, 0.f};
+        const f32x2 fx2 = {x, x}, fy2 = {y, y};
+        auto pair2 = [&](f32x2 ox, f32x2 oy) {
+            const f32x2 dx = fx2 - ox, dy = fy2 - oy;
+            const f32x2 r2 = dx * dx + dy * dy;
+            const f32x2 den = 0.5f + 0.5f * r2;
+            const f32x2 inv = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+            cv2 += 0.8f * inv;
+            const f32x2 i2 = inv * inv;
+            ax2 += (-0.8f * dx) * i2;
+            ay2 += (-0.8f * dy) * i2;
+        };
+        for (int c = 0; c < nq; ++c) {
+            const f32x4 p0 = o4[2 * c], p1 = o4[2 * c + 1];
+            pair2(p0.xy, p0.zw);
+            pair2(p1.xy, p1.zw);
+        }
+        cv = cv2.x + cv2.y;
+        ax = ax2.x + ax2.y;
+        ay = ay2.x + ay2.y;
+    };
+    if constexpr (!WHOLE) {
+        float Cx = 0.f, Cy = 0.f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            Cx += xs[d];
+            Cy += ys[d];
+            w.jx[d] = (xs[d] + Sx) - Cx;
+            w.jy[d] = (ys[d] + Sy) - Cy;
+        }
+        potential(fx, fy, w.cv, w.gx, w.gy);
+    } else {
+        float cvt = 0.f, gxj[D], gyj[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            float cvj;
+            potential(px[j], py[j], cvj, gxj[j], gyj[j]);
+            cvt += cvj;
+        }
+        float GX = 0.f, GY = 0.f, acc = 0.f;
+#pragma unroll
+        for (int l = D - 1; l >= 0; --l) {
+            GX += gxj[l];
+            GY += gyj[l];
+            acc += xs[l] * GX + ys[l] * GY;
+            w.jx[l] = acc;
+            w.jy[l] = 0.f;
+        }
+        w.cv = cvt;
+        w.gx = 1.f;
+        w.gy = 0.f;
     }
-    const float cv = cv2.x + cv2.y, ax = ax2.x + ax2.y, ay = ay2.x + ay2.y;
-    w.cv = cv;
-    w.gx = ax;
-    w.gy = ay;
     float jp = 0.f, jv = 0.f, tx = -INFINITY, tn = INFINITY, va = 0.f;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
@@ -274,6 +305,14 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
     w.tx = tx;
     w.tn = tn;
     w.va = va;
+}
+
+// eval_waypoint with the cost variant chosen at run time (host-API kernels, DynShape optimiser).
+template <int D>
+__device__ __forceinline__ void eval_waypoint_rt(const KParams& P, const float (&q)[D], const float (&v)[D],
+                                                 const float* __restrict__ ob, WP<D>& w) {
+    if (P.whole_robot) eval_waypoint<D, true>(P, q, v, ob, w);
+    else eval_waypoint<D, false>(P, q, v, ob, w);
 }
 
 // Gradient inputs a (→ Kᵀ) and b (→ dKᵀ) of one waypoint, trajectory.py:91-126
@@ -563,11 +602,13 @@ template <int D_, int N_, int RP_>
 struct FixShape {
     static constexpr int D = D_, N = N_, NK = (N_ + 15) / 16 * 16, MP = 2 * NK, RP = RP_;
     static constexpr int NW = (N_ + 63) / 64 * 64, WPT = NW / 64, NSPLIT = stage1_splits(NK);
+    static constexpr bool kVariants = false;  // end-effector cost only (the reference's)
     __device__ explicit FixShape(const KParams&) {}
 };
 template <int D_>
 struct DynShape {
     static constexpr int D = D_;
+    static constexpr bool kVariants = true;  // cost variants chosen at run time (whole_robot)
     int N, NK, MP, RP, NW, WPT, NSPLIT;
     __device__ explicit DynShape(const KParams& P)
         : N(P.N), NK(P.NK), MP(P.MP), RP(P.RP), NW(P.NW), WPT(P.NW >> 6), NSPLIT(P.nsplit) {}
@@ -1039,7 +1080,10 @@ __global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
         const bool ev = (phase != PH_DONE);  // wave-uniform
         WP<D> w;
         if (ev) {
-            if (valid) eval_waypoint<D>(P, q2, v2, obs, w);
+            if (valid) {
+                if constexpr (S::kVariants) eval_waypoint_rt<D>(P, q2, v2, obs, w);
+                else eval_waypoint<D>(P, q2, v2, obs, w);
+            }
             IRM_STAMP(8);
             const float us = P.one_m_lmax * (w.cv * P.invN) + ljl * ((w.jp + w.jv) * P.invN);
             ered_store(valid, w.cv, us, w.tx, w.tn, w.va, phase == PH_RESYNC, n0, red, wave);
@@ -1273,7 +1317,7 @@ __global__ __launch_bounds__(MAXT) void k_forward(KParams P, int mode) {
     }
     WP<D> w;
     if (tvalid) {
-        if (valid) eval_waypoint<D>(P, q, v, obsL, w);
+        if (valid) eval_waypoint_rt<D>(P, q, v, obsL, w);
         eval_partials<D>(P, valid, w, n, wave, q, v, s, g, red, sg, t);
     }
     __syncthreads();
@@ -1348,6 +1392,29 @@ __global__ void k_fk(KParams P, const float* traj, float* pos, float* jac) {
         Cy += ys[d];
         jac[(((size_t)b * 2 + 0) * N + n) * D + d] = (xs[d] + Sx) - Cx;
         jac[(((size_t)b * 2 + 1) * N + n) * D + d] = (ys[d] + Sy) - Cy;
+    }
+}
+
+// robot.py:39-72 (fk_joint_j, generalised to j = 1..D) for B×N waypoints:
+// pos[b][j−1] = (Σ_{l<j} L_l cos c_l, Σ_{l<j} L_l sin c_l), B×D×2×N.
+template <int D>
+__global__ void k_fk_joints(KParams P, const float* traj, float* pos) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int N = P.N;
+    if (i >= P.B * N) return;
+    const int b = i / N, n = i - b * N;
+    const float* q = traj + (size_t)i * D;
+    float cum = 0.f, fx = 0.f, fy = 0.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        cum += q[d];
+        float sn, cs;
+        sincos_fast(cum, sn, cs);
+        fx += P.link[d] * cs;
+        fy += P.link[d] * sn;
+        float* o = pos + (((size_t)b * D + d) * 2) * N + n;
+        o[0] = fx;
+        o[N] = fy;
     }
 }
 
@@ -1451,7 +1518,7 @@ hipError_t launch_optimize(const KParams& p, hipStream_t s) {
         });
     };
     // shape-specialised kernels for the common configurations (auto rank R = 32)
-    if (p.RP == 32 && p.nsplit == stage1_splits(p.NK)) {
+    if (p.RP == 32 && p.nsplit == stage1_splits(p.NK) && !p.whole_robot) {
         if (p.D == 3 && p.N == 50) return run(type_tag<FixShape<3, 50, 32>>{});
         if (p.D == 3 && p.N == 64) return run(type_tag<FixShape<3, 64, 32>>{});
         if (p.D == 3 && p.N == 128) return run(type_tag<FixShape<3, 128, 32>>{});
@@ -1484,6 +1551,16 @@ hipError_t launch_fk(const KParams& p, const float* traj, float* pos, float* jac
     return dispatch_d(p.D, [&](auto dc) {
         constexpr int DD = decltype(dc)::value;
         hipLaunchKernelGGL(k_fk<DD>, dim3((n + 255) / 256), dim3(256), 0, s, p, traj, pos, jac);
+        return hipGetLastError();
+    });
+}
+
+hipError_t launch_fk_joints(const KParams& p, const float* traj, float* pos, hipStream_t s) {
+    const int n = p.B * p.N;
+    if (n <= 0) return hipSuccess;
+    return dispatch_d(p.D, [&](auto dc) {
+        constexpr int DD = decltype(dc)::value;
+        hipLaunchKernelGGL(k_fk_joints<DD>, dim3((n + 255) / 256), dim3(256), 0, s, p, traj, pos);
         return hipGetLastError();
     });
 }

@@ -76,7 +76,8 @@ struct KParams {
     float* series;
     // cost weights of the current call (optimiser: lam_max = --lambda-max-cost)
     float lam_sg, lam_jl, lam_max, one_m_lmax;  // one_m_lmax = fp32(1 − λmax in double)
-    int32_t which, pad2;
+    int32_t which;
+    int32_t whole_robot;  // obstacle cost over every joint position (irm_params.whole_robot_cost)
     float* out0;   // evaluate: B×N×D; cost: B; constraints report: B×11
     float* out1;   // grad: B×N×D
     uint8_t* out_ok;
@@ -184,6 +185,7 @@ hipError_t launch_init_alpha(const KParams& p, float* alpha_out, hipStream_t s);
 hipError_t launch_optimize(const KParams& p, hipStream_t s);
 hipError_t launch_forward(const KParams& p, int mode, hipStream_t s);  // mode: 0 evaluate, 1 cost, 2 cost+grad, 3 constraints
 hipError_t launch_fk(const KParams& p, const float* traj, float* pos, float* jac, hipStream_t s);
+hipError_t launch_fk_joints(const KParams& p, const float* traj, float* pos, hipStream_t s);
 hipError_t launch_cost_vg(const KParams& p, const float* f, float* cv, float* cg, hipStream_t s);
 
 }  // namespace irm

@@ -7,7 +7,7 @@ the stdout lines ("setup object, jit-compile took", "took X ms",
 files trajectory_result.txt / trajectory_series.txt (np.savetxt defaults).
 
 Additive flags (no reference counterpart): --batch-size, --seed,
---operator-rank, --device.
+--operator-rank, --device, --whole-robot-cost.
 """
 import argparse
 import time
@@ -105,6 +105,9 @@ def build_parser():
     parser.add_argument('--operator-rank', type=int, default=0,
                         help="Kernel-operator rank inside the loop: 0 auto, -1 dense exact (default: 0)")
     parser.add_argument('--device', type=int, default=0, help="HIP device ordinal (default: 0)")
+    parser.add_argument('--whole-robot-cost', type=_bool, default=False,
+                        help="Obstacle cost summed over every joint position instead of the end effector only "
+                             "(blog 'Complete Robot Obstacle Avoidance'; default: False)")
     return parser
 
 

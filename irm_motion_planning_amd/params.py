@@ -63,6 +63,7 @@ def params_from_args(args, **overrides):
         "record_series": 0,
         "max_series": 0,
         "traj_per_block": 0,
+        "whole_robot_cost": 0,
     }
     for k, v in knobs.items():
         val = overrides.get(k, getattr(args, k, v))

@@ -1,7 +1,8 @@
 """Planar serial arm — mirrors robot.py of the reference.
 
 fk / jacobian (robot.py:29-36, 75-87) run in the HIP kernel k_fk through
-irm_fk.  The constraint predicates (robot.py:90-113) compare a handful of
+irm_fk; fk_joint_1..3 (robot.py:39-72, any joint 1..D) in k_fk_joints through
+irm_fk_joints.  The constraint predicates (robot.py:90-113) compare a handful of
 norms/extrema of arrays the caller already holds; constraintsFulfilled on a
 whole α runs on the device (irm_constraints).
 """
@@ -27,6 +28,23 @@ class Robot:
     def fk(self, config):
         """End-effector (x, y) per waypoint: (2, N)."""
         return self._ctx.fk(np.asarray(config, np.float32).reshape(-1, self.N_joints))
+
+    def fk_joint(self, config, joint_id):
+        """Position of joint `joint_id` (FK of the first joint_id links): (2, N) — robot.py:39-72
+        generalised to 1 ≤ joint_id ≤ D (k_fk_joints through irm_fk_joints)."""
+        if not 1 <= int(joint_id) <= self.N_joints:
+            raise IrmError(f"joint_id must be in 1..{self.N_joints}")
+        pos = self._ctx.fk_joints(np.asarray(config, np.float32).reshape(-1, self.N_joints))
+        return pos[int(joint_id) - 1]
+
+    def fk_joint_1(self, config):  # robot.py:39-48
+        return self.fk_joint(config, 1)
+
+    def fk_joint_2(self, config):  # robot.py:51-60
+        return self.fk_joint(config, 2)
+
+    def fk_joint_3(self, config):  # robot.py:63-72
+        return self.fk_joint(config, 3)
 
     def jacobian(self, config):
         """∂(x, y)/∂q per waypoint: (2, N, D)."""

@@ -202,6 +202,22 @@ void orc_fk(const orc_ctx* c, const float* traj, float* pos) {
     }
 }
 
+/* robot.py:39-72 fk_joint_j (generalised to j = 1..D): FK of the first j links, i.e. the
+   position of joint j (fk_joint_D = fk). */
+void orc_fk_joint(const orc_ctx* c, const float* traj, int32_t j, float* pos) {
+    int N = c->N, D = c->D;
+    for (int n = 0; n < N; ++n) {
+        float cs = 0.f, px = 0.f, py = 0.f;
+        for (int l = 0; l < j; ++l) {
+            cs += traj[n * D + l];
+            px += c->p.link_length[l] * cosf(cs);
+            py += c->p.link_length[l] * sinf(cs);
+        }
+        pos[n] = px;
+        pos[N + n] = py;
+    }
+}
+
 /* robot.py:75-87: x = -L*sin(c); rc_x = x + sum(x) - cumsum(x); y = L*cos(c). */
 void orc_jacobian(const orc_ctx* c, const float* traj, float* jac) {
     int N = c->N, D = c->D;
@@ -247,12 +263,30 @@ void orc_compute_cost_vg(int32_t N, const float* f, const float* obstacles, int3
     }
 }
 
+/* Per-waypoint obstacle potential.  End effector (the reference, trajectory.py:82,115):
+   compute_cost(fk(traj)).  Whole robot (blog "Insights", DevBlog-Theme/blog-post.html:491-498):
+   Σ_{j=1..D} compute_cost(fk_joint_j(traj)), summed in j order. */
+static void point_costs(const orc_ctx* c, const float* traj, const float* obs, int O, float* cv) {
+    int N = c->N;
+    float f[2 * IRM_MAX_TIMESTEPS], cj[IRM_MAX_TIMESTEPS];
+    if (!c->p.whole_robot_cost) {
+        orc_fk(c, traj, f);
+        orc_compute_cost_vg(N, f, obs, O, cv, NULL);
+        return;
+    }
+    for (int j = 1; j <= c->D; ++j) {
+        orc_fk_joint(c, traj, j, f);
+        orc_compute_cost_vg(N, f, obs, O, j == 1 ? cv : cj, NULL);
+        if (j > 1)
+            for (int n = 0; n < N; ++n) cv[n] += cj[n];
+    }
+}
+
 /* trajectory.py:81-88 (+113-117): obstacle cost of one trajectory. */
 static float obstacle_cost(const orc_ctx* c, const float* traj, const float* obs, int O, float lmax) {
     int N = c->N;
-    float f[2 * IRM_MAX_TIMESTEPS], cv[IRM_MAX_TIMESTEPS];
-    orc_fk(c, traj, f);
-    orc_compute_cost_vg(N, f, obs, O, cv, NULL);
+    float cv[IRM_MAX_TIMESTEPS];
+    point_costs(c, traj, obs, O, cv);
     float mx = cv[0], sum = 0.f;
     for (int n = 0; n < N; ++n) {
         if (cv[n] > mx) mx = cv[n];
@@ -262,12 +296,53 @@ static float obstacle_cost(const orc_ctx* c, const float* traj, const float* obs
     return lmax * mx + (1.f - lmax) * avg;
 }
 
+/* Whole-robot gradient: trajectory.py:91-110 + 120-126 applied to every joint position, the
+   Jacobian of fk_joint_j being robot.py:75-87's reverse cumsum over links 0..j-1 (zero for
+   angles k >= j); the max/mean weights come from the summed per-waypoint cost. */
+static void obstacle_cost_g_whole(const orc_ctx* c, const float* traj, const float* obs, int O, float lmax,
+                                  float* grad) {
+    int N = c->N, D = c->D;
+    float f[2 * IRM_MAX_TIMESTEPS], cv[IRM_MAX_TIMESTEPS], cj[IRM_MAX_TIMESTEPS], cg[2 * IRM_MAX_TIMESTEPS];
+    point_costs(c, traj, obs, O, cv);
+    int idx = 0; /* jnp.argmax: first maximal index */
+    for (int n = 1; n < N; ++n)
+        if (cv[n] > cv[idx]) idx = n;
+    float avg_w = (1.f - lmax) * (1.f / (float)N);
+    for (int i = 0; i < N * D; ++i) grad[i] = 0.f;
+    for (int j = 1; j <= D; ++j) {
+        orc_fk_joint(c, traj, j, f);
+        orc_compute_cost_vg(N, f, obs, O, cj, cg);
+        for (int n = 0; n < N; ++n) {
+            float w = lmax * (n == idx ? 1.f : 0.f) + avg_w;
+            float wx = w * cg[n], wy = w * cg[N + n];
+            float cs = 0.f, x[IRM_MAX_JOINTS], y[IRM_MAX_JOINTS], sx = 0.f, sy = 0.f;
+            for (int l = 0; l < j; ++l) {
+                cs += traj[n * D + l];
+                x[l] = -(c->p.link_length[l] * sinf(cs));
+                y[l] = c->p.link_length[l] * cosf(cs);
+                sx += x[l];
+                sy += y[l];
+            }
+            float cx = 0.f, cy = 0.f;
+            for (int k = 0; k < j; ++k) {
+                cx += x[k];
+                cy += y[k];
+                grad[n * D + k] += wx * ((x[k] + sx) - cx) + wy * ((y[k] + sy) - cy);
+            }
+        }
+    }
+}
+
 /* trajectory.py:91-110 + 120-126: obstacle gradient w.r.t. waypoints. */
 static void obstacle_cost_g(const orc_ctx* c, const float* traj, const float* obs, int O, float lmax,
                             float* grad) {
     int N = c->N, D = c->D;
     float f[2 * IRM_MAX_TIMESTEPS], cv[IRM_MAX_TIMESTEPS], cg[2 * IRM_MAX_TIMESTEPS];
     float jac[2 * IRM_MAX_TIMESTEPS * IRM_MAX_JOINTS];
+    if (c->p.whole_robot_cost) {
+        obstacle_cost_g_whole(c, traj, obs, O, lmax, grad);
+        return;
+    }
     orc_fk(c, traj, f);
     orc_compute_cost_vg(N, f, obs, O, cv, cg);
     int idx = 0; /* jnp.argmax: first maximal index */

@@ -30,6 +30,7 @@ void orc_default_jac(int32_t D, float jgm, uint32_t seed, float* jac_out);
 
 void orc_evaluate(const orc_ctx* c, const float* alpha, int32_t which, float* out);
 void orc_fk(const orc_ctx* c, const float* traj, float* pos);
+void orc_fk_joint(const orc_ctx* c, const float* traj, int32_t j, float* pos);
 void orc_jacobian(const orc_ctx* c, const float* traj, float* jac);
 void orc_compute_cost_vg(int32_t N, const float* f, const float* obstacles, int32_t O, float* cost_v,
                          float* cost_g);

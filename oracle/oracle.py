@@ -39,6 +39,7 @@ def _load():
         lib.orc_default_jac.argtypes = [ctypes.c_int32, ctypes.c_float, ctypes.c_uint32, _fp]
         lib.orc_evaluate.argtypes = [ctypes.c_void_p, _fp, ctypes.c_int32, _fp]
         lib.orc_fk.argtypes = [ctypes.c_void_p, _fp, _fp]
+        lib.orc_fk_joint.argtypes = [ctypes.c_void_p, _fp, ctypes.c_int32, _fp]
         lib.orc_jacobian.argtypes = [ctypes.c_void_p, _fp, _fp]
         lib.orc_compute_cost_vg.argtypes = [ctypes.c_int32, _fp, _fp, ctypes.c_int32, _fp, _fp]
         lib.orc_cost.restype = ctypes.c_float
@@ -115,6 +116,11 @@ class Oracle:
     def fk(self, traj):
         out = np.zeros((2, self.N), np.float32)
         _load().orc_fk(self._c, _p(_f(traj)), _p(out))
+        return out
+
+    def fk_joint(self, traj, j):
+        out = np.zeros((2, self.N), np.float32)
+        _load().orc_fk_joint(self._c, _p(_f(traj)), int(j), _p(out))
         return out
 
     def jacobian(self, traj):

@@ -224,3 +224,43 @@ def test_fp32_alpha_drift():
     a32, _ = o1.optimize(a0, obs, s[0], g[0])
     a64, _, _ = r.gd_single(a0, obs, s[0], g[0], 1)
     assert np.abs(o1.evaluate(a32) - r.traj_vel(a64)[0]).max() < 2e-3
+
+
+# ------------------------------------------------ whole-robot cost
+
+@pytest.fixture(scope="session")
+def g_wr():
+    from conftest import golden
+    return golden("ref_whole_robot_n50")
+
+
+@pytest.mark.parametrize("name", ["alpha0", "small1", "small2"])
+def test_oracle_fk_joint_matches_reference(g_wr, name):
+    """Robot.fk_joint_1..3 (robot.py:39-72) of the golden trajectories; fk_joint_3 = fk."""
+    o = oracle_for()
+    tr = g_wr[f"traj_{name}"]
+    for j in (1, 2, 3):
+        np.testing.assert_allclose(o.fk_joint(tr, j), g_wr[f"fkj_{name}"][j - 1], rtol=0, atol=1e-6)
+    np.testing.assert_array_equal(o.fk_joint(tr, 3), o.fk(tr))
+
+
+@pytest.mark.parametrize("name", ["small1", "small2", "alpha0"])
+def test_oracle_whole_robot_cost_and_grad(g_wr, g_eval, name):
+    """Σ_j compute_cost(fk_joint_j) composed from the reference's functions (gen_golden_whole_robot.py):
+    the oracle's α-space cost equals the golden loss, and its α-space gradient equals
+    Kᵀ·(d loss/d traj)·Jᵀ of the golden fp64 finite differences."""
+    o = oracle_for(whole_robot_cost=1)
+    _, K, _, J = o.kernel_matrices()
+    a = g_eval[name]
+    obs = g_wr["obstacles"]
+    # α0's waypoints carry the reference's fp32 evaluation noise (5e-4, SURVEY.md A.1)
+    rtol, gtol = (2e-3, 5e-3) if name == "alpha0" else (1e-5, 2e-4)
+    for i, lm in enumerate(g_wr["lmax"]):
+        c = o.cost(a, obs, START, GOAL, 0, 0, float(lm))
+        ref = float(g_wr[f"loss_{name}"][i])
+        assert abs(c - ref) <= rtol * abs(ref), (lm, c, ref)
+        G = o.cost_g(a, obs, START, GOAL, 0, 0, float(lm))
+        Gref = K.T.astype(np.float64) @ g_wr[f"grad_{name}"][i].astype(np.float64) @ J.T.astype(np.float64)
+        assert np.abs(G - Gref).max() <= gtol * np.abs(Gref).max(), (lm, np.abs(G - Gref).max())
+    # the end-effector cost is one of the summands: whole robot ≥ end effector
+    assert o.cost(a, obs, START, GOAL, 0, 0, 0.0) > oracle_for().cost(a, obs, START, GOAL, 0, 0, 0.0)
