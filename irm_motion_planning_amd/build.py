@@ -1,31 +1,30 @@
 """In-tree build of libirm_hip.so (hipcc, gfx950 only).
 
-    python -m irm_motion_planning_amd.build [--force]
+    python -m irm_motion_planning_amd.build [--force] [--prof] [-j N]
 
-The .so lands next to this file so that it travels with the repository
-snapshot to the GPU box (it is git-ignored, not gpurun-ignored).
+The optimiser templates (csrc/irm_kernels_impl.hpp) are instantiated in one
+object per problem shape (csrc/irm_opt_inst.hip compiled with IRM_INST_*), so
+the objects build in parallel; the host-API kernels and dispatch
+(irm_kernels.hip) and the C ABI (irm_host.cpp) are two more objects.  The .so
+lands next to this file so that it travels with the repository snapshot to the
+GPU box (it is git-ignored, not gpurun-ignored); objects stay in _obj/.
 """
 import os
 import subprocess
 import sys
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
+OBJ = os.path.join(HERE, "_obj")
 OUT = os.path.join(HERE, "libirm_hip.so")
-SOURCES = ["irm_kernels.hip", "irm_host.cpp"]
-HEADERS = ["irm_kernels.hpp", os.path.join("..", "..", "include", "irm.h")]
+HEADERS = [os.path.join(CSRC, h) for h in ("irm_kernels.hpp", "irm_kernels_impl.hpp")] + \
+    [os.path.join(HERE, "..", "include", "irm.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-Wall", "-Wno-unused-function"]
-
-
-def _stale():
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS] + [__file__]
-    return any(os.path.getmtime(d) > t for d in deps)
-
+CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-unused-function"]
+FIX_SHAPES = [(3, 50), (3, 64), (3, 128), (3, 256), (7, 256)]  # IRM_FIX_SHAPES in irm_kernels_impl.hpp
+MAX_D = 8
 
 VARIANTS = {
     "": ("libirm_hip.so", []),
@@ -33,31 +32,59 @@ VARIANTS = {
 }
 
 
-def build(force=False, verbose=False, variant=""):
+def units():
+    """(object name, source, extra flags) of every compilation unit."""
+    u = [("irm_kernels", "irm_kernels.hip", []), ("irm_host", "irm_host.cpp", [])]
+    u += [(f"opt_dyn{d}", "irm_opt_inst.hip", [f"-DIRM_INST_DYN={d}"]) for d in range(1, MAX_D + 1)]
+    u += [(f"opt_fix{d}_{n}", "irm_opt_inst.hip", [f"-DIRM_INST_FIX_D={d}", f"-DIRM_INST_FIX_N={n}"])
+          for d, n in FIX_SHAPES]
+    return u
+
+
+def _newer(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=False, variant="", jobs=None):
     name, extra = VARIANTS[variant]
     out = os.path.join(HERE, name)
-    if variant:
-        cmd = [HIPCC] + FLAGS + extra + ["-o", out] + [os.path.join(CSRC, s) for s in SOURCES]
+    odir = os.path.join(OBJ, variant or "release")
+    os.makedirs(odir, exist_ok=True)
+    jobs = jobs or min(16, os.cpu_count() or 1)
+    todo, objs = [], []
+    for oname, src, flags in units():
+        obj = os.path.join(odir, oname + ".o")
+        objs.append(obj)
+        deps = [os.path.join(CSRC, src), __file__] + HEADERS
+        if force or _newer(obj, deps):
+            todo.append([HIPCC] + CFLAGS + extra + flags + ["-c", "-o", obj, os.path.join(CSRC, src)])
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd, cwd=CSRC)
-        return out
-    if not force and not _stale():
-        return OUT
-    cmd = [HIPCC] + FLAGS + ["-o", OUT] + [os.path.join(CSRC, s) for s in SOURCES]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    subprocess.check_call(cmd, cwd=CSRC)
-    return OUT
+
+    if todo:
+        with ThreadPoolExecutor(jobs) as ex:
+            list(ex.map(run, todo))
+    if todo or force or _newer(out, objs):
+        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs)
+    return out
 
 
-def asm(out_dir):
-    """Emit the gfx950 assembly of the kernels (for ISA inspection)."""
+def asm(out_dir, inst=("-DIRM_INST_FIX_D=3", "-DIRM_INST_FIX_N=128")):
+    """Emit the gfx950 assembly of one instantiation unit (for ISA inspection)."""
     os.makedirs(out_dir, exist_ok=True)
-    cmd = [HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "--cuda-device-only", "-S",
-           "-o", os.path.join(out_dir, "irm_kernels.s"), os.path.join(CSRC, "irm_kernels.hip")]
+    cmd = [HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "--cuda-device-only", "-S", *inst,
+           "-o", os.path.join(out_dir, "irm_opt.s"), os.path.join(CSRC, "irm_opt_inst.hip")]
     subprocess.check_call(cmd, cwd=CSRC)
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, verbose=True)
+    jobs = int(sys.argv[sys.argv.index("-j") + 1]) if "-j" in sys.argv else None
+    build(force="--force" in sys.argv, verbose=True, jobs=jobs)
     if "--prof" in sys.argv:
-        build(variant="prof", verbose=True)
+        build(force="--force" in sys.argv, variant="prof", verbose=True, jobs=jobs)

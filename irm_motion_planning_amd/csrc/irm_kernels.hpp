@@ -164,7 +164,32 @@ __host__ __device__ constexpr Head plan_head(int MP, int RP, int nsplit, bool op
     return H;
 }
 
-__host__ __device__ Plan plan_lds(const KParams& p, bool ops_lds, bool optimizer);
+__host__ __device__ inline Plan plan_lds(const KParams& p, bool ops_lds, bool optimizer) {
+    const Head H = plan_head(p.MP, p.RP, p.nsplit, optimizer);
+    Plan L{};
+    L.X = H.X;
+    L.Bs = L.X + p.NK * kLd;
+    L.dP = H.dP;
+    L.Ypart = H.Ypart;
+    L.Ymix = H.Ymix;
+    L.Ydir = L.Yacc = L.alist = L.acnt = L.act = L.list = L.fb = 0;
+    L.red = H.red;
+    L.sg = H.sg;
+    L.wp = H.wp;
+    L.flags = H.flags;
+    L.obs = H.obs;
+    int off = H.obs + al4((p.obs_stride ? p.TB : 1) * ((p.O + 3) & ~3) * 2 + 4);
+    L.f1 = L.f2 = 0;
+    if (optimizer && ops_lds && !p.regops) {  // with REGOPS the A-fragments live in VGPRs
+        L.f1 = off;
+        off += al4((int)frag_floats(p.RP, p.MP));
+        L.f2 = off;
+        off += al4((int)frag_floats(p.MP, p.RP));
+    }
+    L.total = off;
+    return L;
+}
+
 
 // Stage-1 split-K factor: units of 4 k-quads over the position half.
 __host__ __device__ constexpr int stage1_splits(int NK) { return (NK / 16 + 3) / 4; }

@@ -1,0 +1,1420 @@
+// irm_kernels_impl.hpp — gfx950 (CDNA4) kernel templates of the RKHS trajectory optimiser.
+// Included by irm_kernels.hip (host-API kernels, launch dispatch) and by the instantiation
+// units irm_opt_inst.hip (one k_optimize shape / k_forward D per object, compiled in parallel).
+//
+// Hot path of simongroeger/irm_motion_planning: optimizer_GD.py:386-445 and
+// optimizer_BLS.py:126-213 over trajectory.py:271-297 / robot.py:29-87 /
+// environment.py:32-58.  DESIGN.md describes the formulation:
+//   * the optimiser state is kept in trajectory space, T = K·α·J and
+//     V = dK·α·J (the reference keeps α, |α|≈1e3, which cancels in fp32);
+//   * the α-space step α' = c·α − s·G, G = (Kᵀa + dKᵀb)Jᵀ, becomes
+//     [T';V'] = c·[T;V] − s·L·Lᵀ[a;b]·JᵀJ with L = [K;dK];
+//   * L·Lᵀ is applied as F·(Fᵀ[a;b]) with F = L·V_R (V_R = top-R right
+//     singular vectors of L; R = N, V = I is the exact dense operator);
+//   * both contractions run on v_mfma_f32_16x16x4_f32 with the TB·D
+//     (trajectory, joint) columns of a workgroup as the 16 MFMA columns;
+//   * one lane per (trajectory, waypoint): the trajectory's waypoints and
+//     velocities live in that lane's registers for the whole optimisation;
+//     FK / obstacle potential / penalties are VALU, per-trajectory
+//     reductions are DPP wave reductions + a cross-wave LDS combine;
+//   * the GD / BLS control flow is a per-trajectory state machine whose
+//     scalar state is replicated in the trajectory's lanes (every lane takes
+//     the same decision from the same reduced values), inside one persistent
+//     launch per optimize().
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "irm_kernels.hpp"
+
+namespace irm {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// ------------------------------------------------------------ LDS planning
+
+// ------------------------------------------------------------ wave helpers
+// DPP row reductions (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+// row_mirror) leave each 16-lane row reduced in all its lanes; the four
+// rows are then combined from v_readlane (uniform result, no LDS).
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dppi(int v) {
+    return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ float lanef(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float wred_sum(float v) {
+    v += dppf<0xB1>(v);
+    v += dppf<0x4E>(v);
+    v += dppf<0x141>(v);
+    v += dppf<0x140>(v);
+    return (lanef(v, 0) + lanef(v, 16)) + (lanef(v, 32) + lanef(v, 48));
+}
+__device__ __forceinline__ float wred_max(float v) {
+    v = fmaxf(v, dppf<0xB1>(v));
+    v = fmaxf(v, dppf<0x4E>(v));
+    v = fmaxf(v, dppf<0x141>(v));
+    v = fmaxf(v, dppf<0x140>(v));
+    return fmaxf(fmaxf(lanef(v, 0), lanef(v, 16)), fmaxf(lanef(v, 32), lanef(v, 48)));
+}
+__device__ __forceinline__ float wred_min(float v) {
+    v = fminf(v, dppf<0xB1>(v));
+    v = fminf(v, dppf<0x4E>(v));
+    v = fminf(v, dppf<0x141>(v));
+    v = fminf(v, dppf<0x140>(v));
+    return fminf(fminf(lanef(v, 0), lanef(v, 16)), fminf(lanef(v, 32), lanef(v, 48)));
+}
+// max with first-index tie break (jnp.argmax, trajectory.py:97)
+__device__ __forceinline__ void amax_step(float& v, int& i, float ov, int oi) {
+    if (ov > v || (ov == v && oi < i)) {
+        v = ov;
+        i = oi;
+    }
+}
+template <int CTRL>
+__device__ __forceinline__ void amax_dpp(float& v, int& i) {
+    float ov = dppf<CTRL>(v);
+    int oi = dppi<CTRL>(i);
+    amax_step(v, i, ov, oi);
+}
+__device__ __forceinline__ void wred_argmax(float& v, int& i) {
+    amax_dpp<0xB1>(v, i);
+    amax_dpp<0x4E>(v, i);
+    amax_dpp<0x141>(v, i);
+    amax_dpp<0x140>(v, i);
+    float bv = lanef(v, 0);
+    int bi = __builtin_amdgcn_readlane(i, 0);
+#pragma unroll
+    for (int r = 16; r < 64; r += 16) amax_step(bv, bi, lanef(v, r), __builtin_amdgcn_readlane(i, r));
+    v = bv;
+    i = bi;
+}
+
+// ---------------------------------------------------- phase profiler (diag)
+// Built with -DIRM_PHASE_PROFILE: thread 0 of each workgroup accumulates the
+// shader-clock cycles (s_memtime) between consecutive stamps per phase into
+// P.prof[block][phase].  In the shipped build every stamp is empty.
+struct Prof {
+#ifdef IRM_PHASE_PROFILE
+    unsigned long long last, acc[kProfPhases];
+    __device__ __forceinline__ void init() {
+        last = __builtin_amdgcn_s_memtime();
+#pragma unroll
+        for (int i = 0; i < kProfPhases; ++i) acc[i] = 0;
+    }
+    __device__ __forceinline__ void stamp(int ph) {
+        unsigned long long now = __builtin_amdgcn_s_memtime();
+        acc[ph] += now - last;
+        last = now;
+    }
+    __device__ __forceinline__ void flush(unsigned long long* out) {
+        if (out)
+            for (int i = 0; i < kProfPhases; ++i) out[(size_t)blockIdx.x * kProfPhases + i] = acc[i];
+    }
+#else
+    __device__ __forceinline__ void init() {}
+    __device__ __forceinline__ void stamp(int) {}
+    __device__ __forceinline__ void flush(unsigned long long*) {}
+#endif
+};
+#ifdef IRM_ISA_MARKS  // analysis builds: phase markers in the emitted assembly
+#define IRM_STAMP(ph) asm volatile("; IRM_PHASE " #ph)
+#else
+#define IRM_STAMP(ph)                         \
+    do {                                      \
+        if (threadIdx.x == 0) prof.stamp(ph); \
+    } while (0)
+#endif
+
+// ---------------------------------------------------------- MFMA contraction
+// D layout of 16x16x4: lane l holds rows 4*(l>>4)+i, column l&15.
+// Callers keep every tile inside the buffer (row extents are multiples of 16).
+__device__ __forceinline__ void store_tile(float* out, int tile, f32x4 acc, unsigned colmask) {
+    const int lane = threadIdx.x & 63;
+    const int col = lane & 15;
+    if (!((colmask >> col) & 1u)) return;
+    float* o = out + (tile * 16 + 4 * (lane >> 4)) * kLd + col;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i * kLd] = acc[i];
+}
+
+// ------------------------------------------------ per-waypoint physics
+// sin/cos for robot.py's joint angles: Cody-Waite reduction by π/2 (3-part
+// split, fma) and the cephes single-precision minimax polynomials on
+// [−π/4, π/4]; ≈1 ulp, branch-free.  |x| > 1e4 rad falls back to sincosf.
+__device__ __forceinline__ void sincos_fast(float x, float& sn, float& cs) {
+    if (__builtin_expect(fabsf(x) > 1.0e4f, 0)) {
+        sincosf(x, &sn, &cs);
+        return;
+    }
+    const float kf = rintf(x * 0.636619772f);
+    float r = fmaf(kf, -1.57079637050628662109375f, x);
+    r = fmaf(kf, 4.371138828673793e-08f, r);
+    r = fmaf(kf, 1.7151245100058819e-15f, r);
+    const float z = r * r;
+    const float sp = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
+    const float cp = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f), 4.166664568298827e-2f),
+                          fmaf(-0.5f, z, 1.0f));
+    const int q = (int)kf & 3;
+    const float s0 = (q & 1) ? cp : sp;
+    const float c0 = (q & 1) ? sp : cp;
+    sn = (q & 2) ? -s0 : s0;
+    cs = ((q + 1) & 2) ? -c0 : c0;
+}
+
+template <int D>
+struct WP {
+    float cv, gx, gy;        // obstacle potential and its gradient at the end effector
+    float jp, jv;            // masked joint-position / joint-velocity penalty terms
+    float tx, tn, va;        // max/min joint position, max |joint velocity|
+    float jx[D], jy[D];      // end-effector Jacobian row
+};
+
+// robot.py:29-36 (fk), 75-87 (jacobian); environment.py:46-58
+// (compute_cost_vg); trajectory.py:215-227, 245-255 (penalty elements).
+// WHOLE: the potential is summed over every joint position p_j = fk_joint_j
+// (robot.py:39-72; DevBlog-Theme/blog-post.html:491-498) instead of the end
+// effector only.  Its gradient w.r.t. angle k is Σ_{l≥k} (X_l·GX_l + Y_l·GY_l)
+// with (X_l, Y_l) = L_l·(−sin c_l, cos c_l) and GX_l = Σ_{j≥l} ∂cost/∂p_j; it is
+// returned as w.jx (with w.gx = 1, w.jy = w.gy = 0) so grad_waypoint is shared.
+template <int D, bool WHOLE = false>
+__device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)[D], const float (&v)[D],
+                                              const float* __restrict__ ob, WP<D>& w) {
+    float cum = 0.f, fx = 0.f, fy = 0.f, Sx = 0.f, Sy = 0.f;
+    float xs[D], ys[D], px[D], py[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        cum += q[d];
+        float sn, cs;
+        sincos_fast(cum, sn, cs);
+        fx += P.link[d] * cs;
+        fy += P.link[d] * sn;
+        px[d] = fx;
+        py[d] = fy;
+        xs[d] = -(P.link[d] * sn);
+        ys[d] = P.link[d] * cs;
+        Sx += xs[d];
+        Sy += ys[d];
+    }
+    // Obstacles are staged in LDS in pairs (x_a, x_b, y_a, y_b), padded to a multiple of 4
+    // with sentinels at (1e20, 1e20): r² overflows to +inf, rcp → 0, so a sentinel adds
+    // exactly 0.  Two obstacles per packed-fp32 instruction; the even- and odd-numbered
+    // obstacles accumulate separately and are added at the end.
+    const f32x4* o4 = reinterpret_cast<const f32x4*>(ob);
+    const int nq = (P.O + 3) >> 2;
+    auto potential = [&](float x, float y, float& cv, float& ax, float& ay) {
+        f32x2 cv2 = {0.f, 0.f}, ax2 = {0.f, 0.f}, ay2 = {0.f, 0.f};
+        const f32x2 fx2 = {x, x}, fy2 = {y, y};
+        auto pair2 = [&](f32x2 ox, f32x2 oy) {
+            const f32x2 dx = fx2 - ox, dy = fy2 - oy;
+            const f32x2 r2 = dx * dx + dy * dy;
+            const f32x2 den = 0.5f + 0.5f * r2;
+            const f32x2 inv = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+            cv2 += 0.8f * inv;
+            const f32x2 i2 = inv * inv;
+            ax2 += (-0.8f * dx) * i2;
+            ay2 += (-0.8f * dy) * i2;
+        };
+        for (int c = 0; c < nq; ++c) {
+            const f32x4 p0 = o4[2 * c], p1 = o4[2 * c + 1];
+            pair2(p0.xy, p0.zw);
+            pair2(p1.xy, p1.zw);
+        }
+        cv = cv2.x + cv2.y;
+        ax = ax2.x + ax2.y;
+        ay = ay2.x + ay2.y;
+    };
+    if constexpr (!WHOLE) {
+        float Cx = 0.f, Cy = 0.f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            Cx += xs[d];
+            Cy += ys[d];
+            w.jx[d] = (xs[d] + Sx) - Cx;
+            w.jy[d] = (ys[d] + Sy) - Cy;
+        }
+        potential(fx, fy, w.cv, w.gx, w.gy);
+    } else {
+        float cvt = 0.f, gxj[D], gyj[D];
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            float cvj;
+            potential(px[j], py[j], cvj, gxj[j], gyj[j]);
+            cvt += cvj;
+        }
+        float GX = 0.f, GY = 0.f, acc = 0.f;
+#pragma unroll
+        for (int l = D - 1; l >= 0; --l) {
+            GX += gxj[l];
+            GY += gyj[l];
+            acc += xs[l] * GX + ys[l] * GY;
+            w.jx[l] = acc;
+            w.jy[l] = 0.f;
+        }
+        w.cv = cvt;
+        w.gx = 1.f;
+        w.gy = 0.f;
+    }
+    float jp = 0.f, jv = 0.f, tx = -INFINITY, tn = INFINITY, va = 0.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const float z = (q[d] - P.mean_pos) * P.inv_std_pos;
+        const bool m = (q[d] > P.thr_hi) || (q[d] < P.thr_lo);
+        jp += (P.cvdl && !m) ? 0.f : 0.5f * (z * z);
+        const float zv = v[d] * P.inv_vmax;
+        const bool mv = fabsf(v[d]) > P.thr_v;
+        jv += (P.cvdl && !mv) ? 0.f : 0.5f * (zv * zv);
+        tx = fmaxf(tx, q[d]);
+        tn = fminf(tn, q[d]);
+        va = fmaxf(va, fabsf(v[d]));
+    }
+    w.jp = jp;
+    w.jv = jv;
+    w.tx = tx;
+    w.tn = tn;
+    w.va = va;
+}
+
+// eval_waypoint with the cost variant chosen at run time (host-API kernels, DynShape optimiser).
+template <int D>
+__device__ __forceinline__ void eval_waypoint_rt(const KParams& P, const float (&q)[D], const float (&v)[D],
+                                                 const float* __restrict__ ob, WP<D>& w) {
+    if (P.whole_robot) eval_waypoint<D, true>(P, q, v, ob, w);
+    else eval_waypoint<D, false>(P, q, v, ob, w);
+}
+
+// Gradient inputs a (→ Kᵀ) and b (→ dKᵀ) of one waypoint, trajectory.py:91-126
+// (obstacle), 191-212 (start/goal), 231-242 / 259-268 (joint limits).
+template <int D>
+__device__ __forceinline__ void grad_waypoint(const KParams& P, const WP<D>& w, const float (&q)[D],
+                                              const float (&v)[D], int n, int idx, float lsg, float ljl,
+                                              const float (&s)[D], const float (&g)[D], float (&a)[D],
+                                              float (&b)[D]) {
+    const int N = P.N;
+    const float wt = (n == idx ? P.lam_max : 0.f) + P.one_m_lmax * P.invN;
+    const float wx = wt * w.gx, wy = wt * w.gy;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        float sgp = 0.f, sgv = 0.f;
+        if (n == 0) {
+            sgp = q[d] - s[d];
+            sgv = v[d];
+        }
+        if (n == N - 1) {
+            sgp = q[d] - g[d];
+            sgv = v[d];
+        }
+        float jpg = 0.f, jvg = 0.f;
+        const bool m = (q[d] > P.thr_hi) || (q[d] < P.thr_lo);
+        if (!P.cvdl || m) jpg = ((q[d] - P.mean_pos) * P.inv_std2) * P.invN;
+        const bool mv = fabsf(v[d]) > P.thr_v;
+        if (!P.cvdl || mv) jvg = (v[d] * P.inv_vmax2) * P.invN;
+        a[d] = (wx * w.jx[d] + wy * w.jy[d]) + lsg * sgp + ljl * jpg;
+        b[d] = lsg * sgv + ljl * jvg;
+    }
+}
+
+// Result of one cost evaluation of one trajectory (reduced over waypoints).
+struct EvalOut {
+    float loss, ds, dg, vs, vg, tmax, tmin, vabs;
+    int idx;
+};
+
+// Wave-reduce this lane's waypoint terms; lane 0 of each wave stores the
+// partials, the lanes of rows 0 / N−1 store the start/goal terms.  Must be
+// reached by the whole wave (a wave never straddles two trajectories).
+template <int D>
+__device__ __forceinline__ void eval_partials(const KParams& P, bool live, const WP<D>& w, int n, int wave,
+                                              const float (&q)[D], const float (&v)[D], const float (&s)[D],
+                                              const float (&g)[D], float* red, float* sg, int t) {
+    float cmax = live ? w.cv : -INFINITY;
+    int cidx = live ? n : 0x7fffffff;
+    wred_argmax(cmax, cidx);
+    const float csum = wred_sum(live ? w.cv : 0.f);
+    const float jps = wred_sum(live ? w.jp : 0.f);
+    const float jvs = wred_sum(live ? w.jv : 0.f);
+    const float tx = wred_max(live ? w.tx : -INFINITY);
+    const float tn = wred_min(live ? w.tn : INFINITY);
+    const float va = wred_max(live ? w.va : 0.f);
+    if ((threadIdx.x & 63) == 0) {
+        float* r = red + wave * 10;
+        r[0] = cmax;
+        r[1] = __int_as_float(cidx);
+        r[2] = csum;
+        r[3] = jps;
+        r[4] = jvs;
+        r[5] = tx;
+        r[6] = tn;
+        r[7] = va;
+    }
+    if (live && (n == 0 || n == P.N - 1)) {  // trajectory.py:183-204 rows 0 and N−1
+        float a = 0.f, bb = 0.f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const float e = q[d] - (n == 0 ? s[d] : g[d]);
+            a += e * e;
+            bb += v[d] * v[d];
+        }
+        sg[t * 4 + (n == 0 ? 0 : 2)] = a;
+        sg[t * 4 + (n == 0 ? 1 : 3)] = bb;
+    }
+}
+
+// Combine the trajectory's wave partials (fixed order) into loss + stats.
+__device__ __forceinline__ EvalOut eval_finalize(const KParams& P, const float* red, const float* sg, int t,
+                                                 int wave0, int nwt, float lsg, float ljl) {
+    const float* r = red + wave0 * 10;
+    float cmax = r[0];
+    int cidx = __float_as_int(r[1]);
+    float csum = r[2], jps = r[3], jvs = r[4], tx = r[5], tn = r[6], va = r[7];
+    for (int w = 1; w < nwt; ++w) {
+        const float* q = red + (wave0 + w) * 10;
+        amax_step(cmax, cidx, q[0], __float_as_int(q[1]));
+        csum += q[2];
+        jps += q[3];
+        jvs += q[4];
+        tx = fmaxf(tx, q[5]);
+        tn = fminf(tn, q[6]);
+        va = fmaxf(va, q[7]);
+    }
+    const float a0 = sg[t * 4 + 0], b0 = sg[t * 4 + 1], a1 = sg[t * 4 + 2], b1 = sg[t * 4 + 3];
+    const float nN = (float)P.N;
+    const float sgpc = 0.5f * a0 + 0.5f * a1;                          // trajectory.py:187
+    const float sgvc = 0.5f * b0 + 0.5f * b1;                          // trajectory.py:203
+    const float toc = P.lam_max * cmax + P.one_m_lmax * (csum / nN);    // trajectory.py:85-87
+    EvalOut e;
+    e.loss = toc + lsg * (sgpc + sgvc) + ljl * (jps / nN + jvs / nN);  // trajectory.py:281
+    e.idx = cidx;
+    e.ds = sqrtf(a0);
+    e.dg = sqrtf(a1);
+    e.vs = sqrtf(b0);
+    e.vg = sqrtf(b1);
+    e.tmax = tx;
+    e.tmin = tn;
+    e.vabs = va;
+    return e;
+}
+
+// Obstacles into LDS: one shared set (obs_stride 0) or one per trajectory,
+// each padded to obs_pitch floats with zero-contribution sentinels.
+__host__ __device__ inline int obs_pitch(int O) { return ((O + 3) & ~3) * 2; }
+__device__ inline void stage_obstacles(const KParams& P, int tb0, int ntb, float* obsL) {
+    const int pitch = obs_pitch(P.O), nsets = P.obs_stride ? P.TB : 1;
+    for (int e = threadIdx.x; e < nsets * pitch; e += P.BT) {
+        const int tt = e / pitch, r = e - tt * pitch;
+        // r = 4·pair + 2·coord + j  →  obstacle 2·pair + j, coordinate coord
+        const int o = 2 * (r >> 2) + (r & 1), coord = (r >> 1) & 1;
+        float val = 1.0e20f;
+        if (o < P.O) {
+            const int src = 2 * o + coord;
+            if (!P.obs_stride) val = P.obstacles[src];
+            else if (tt < ntb) val = P.obstacles[(size_t)(tb0 + tt) * P.obs_stride + src];
+        }
+        obsL[e] = val;
+    }
+}
+
+// α0 of the block's trajectories into X[n][tD+d] (rows ≥ N / unused columns 0).
+template <int D>
+__device__ void stage_alpha(const KParams& P, int tb0, int ntb, float* X, int xrows) {
+    const int N = P.N;
+    for (int e = threadIdx.x; e < xrows * 16; e += P.BT) {
+        const int n = e >> 4, c = e & 15, t = c / D, d = c - t * D;
+        float* dst = X + n * kLd + c;
+        float val = 0.f;
+        if (n < N && t < ntb) {
+            const size_t b = (size_t)(tb0 + t);
+            if (P.alpha0) {
+                val = P.alpha0[(b * N + n) * D + d];
+            } else {  // trajectory.py:73-78 via K⁻¹(1−c), K⁻¹c (linearity of solve)
+                float sj = 0.f, gj = 0.f;
+                for (int e2 = 0; e2 < D; ++e2) {
+                    sj += P.start[b * D + e2] * P.Jinv[e2 * D + d];
+                    gj += P.goal[b * D + e2] * P.Jinv[e2 * D + d];
+                }
+                val = P.uvec[n] * sj + P.wvec[n] * gj;
+            }
+        }
+        *dst = val;
+    }
+}
+
+// ------------------------------------------- correctly rounded α-space maps
+// The reference's K@α@J (trajectory.py:63-65) contracts over N waypoints with
+// |α| ≈ 1e3 (singular K): a plain fp32 sum carries ~1e-4 (positions) and
+// ~1e-3 (velocities) of order-dependent noise.  Here every product of two
+// fp32 values is exact in fp64 and the N-term sum accumulates in fp64 (same
+// sequential order as oracle/irm_oracle.c), then rounds once — the result is
+// the correctly rounded fp32 value, bit-identical to the CPU oracle.  Used off
+// the hot loop: host-API evaluation and the optimiser's prologue / resyncs.
+//
+// Lane n of trajectory column block Xa (LDS, rows m = 0..N-1, stride kLd):
+//   q = fp32(fp32(K·α)[n]·J), v = fp32(fp32(dK·α)[n]·J).
+template <int D>
+__device__ void eval_exact(const KParams& P, const float* __restrict__ Xa, int n, float (&q)[D], float (&v)[D],
+                           const float* Kt = nullptr, const float* dKt = nullptr) {
+    const int N = P.N;
+    double aq[D], av[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) aq[d] = av[d] = 0.0;
+    const float* kt = (Kt ? Kt : P.Kt) + n;
+    const float* dkt = (dKt ? dKt : P.dKt) + n;
+    for (int m = 0; m < N; ++m) {
+        const double kq = (double)kt[(size_t)m * N], kv = (double)dkt[(size_t)m * N];  // K[n][m], dK[n][m]
+        const float* xr = Xa + m * kLd;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const double x = (double)xr[d];
+            aq[d] = fma(kq, x, aq[d]);
+            av[d] = fma(kv, x, av[d]);
+        }
+    }
+    float tq[D], tv[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        tq[d] = (float)aq[d];
+        tv[d] = (float)av[d];
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        double sq = 0.0, sv = 0.0;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            sq = fma((double)tq[d], (double)P.J[d * D + k], sq);
+            sv = fma((double)tv[d], (double)P.J[d * D + k], sv);
+        }
+        q[k] = (float)sq;
+        v[k] = (float)sv;
+    }
+}
+
+// G[n] = (fp32(Kᵀa)[n] + fp32(dKᵀb)[n])·Jᵀ  (trajectory.py:295), the N-sums
+// in fp64 as above, the fp32 add and the D-term J product unfused in fp32
+// (the oracle's order).  Xa: a in rows 0..N-1, b in rows N..2N-1.
+template <int D>
+__device__ void grad_exact(const KParams& P, const float* __restrict__ Xa, int n, float (&G)[D]) {
+    const int N = P.N;
+    double ga[D], gb[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) ga[d] = gb[d] = 0.0;
+    const float* km = P.Km + n;
+    const float* dkm = P.dKm + n;
+    for (int m = 0; m < N; ++m) {
+        const double ka = (double)km[(size_t)m * N], kb = (double)dkm[(size_t)m * N];  // K[m][n], dK[m][n]
+        const float* xa = Xa + m * kLd;
+        const float* xb = Xa + (N + m) * kLd;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            ga[d] = fma(ka, (double)xa[d], ga[d]);
+            gb[d] = fma(kb, (double)xb[d], gb[d]);
+        }
+    }
+    float tmp[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) tmp[d] = __fadd_rn((float)ga[d], (float)gb[d]);
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        float u = 0.f;
+#pragma unroll
+        for (int l = 0; l < D; ++l) u = __fadd_rn(u, __fmul_rn(tmp[l], P.J[k * D + l]));
+        G[k] = u;
+    }
+}
+
+// ------------------------------------------------------------ optimiser
+// Wave reduction of one evaluation's per-waypoint terms.
+// usum: Σ_n [(1−λmax)/N·cost_v[n] + λjl/N·(jp[n] + jv[n])], the mean-obstacle and
+// joint-limit terms of trajectory.py:281 folded into one sum; cmax with the
+// first-index argmax of jnp.argmax (trajectory.py:97) from a ballot of the lanes
+// holding the wave maximum.  tx/tn/va (constraint extrema) only when `ext`.
+// Lane 0 stores the wave's record at red[wave·8].
+__device__ __forceinline__ void ered_store(bool live, float cv, float us, float tx, float tn, float va, bool ext,
+                                           int n0, float* red, int wave) {
+    float m = live ? cv : -INFINITY, s = live ? us : 0.f;
+    m = fmaxf(m, dppf<0xB1>(m));
+    s += dppf<0xB1>(s);
+    m = fmaxf(m, dppf<0x4E>(m));
+    s += dppf<0x4E>(s);
+    m = fmaxf(m, dppf<0x141>(m));
+    s += dppf<0x141>(s);
+    m = fmaxf(m, dppf<0x140>(m));
+    s += dppf<0x140>(s);
+    const float wm = fmaxf(fmaxf(lanef(m, 0), lanef(m, 16)), fmaxf(lanef(m, 32), lanef(m, 48)));
+    const float ws = (lanef(s, 0) + lanef(s, 16)) + (lanef(s, 32) + lanef(s, 48));
+    const unsigned long long hit = __ballot(live && cv == wm);
+    const int idx = hit ? n0 + __builtin_ctzll(hit) : 0x7fffffff;
+    float ox = 0.f, on = 0.f, oa = 0.f;
+    if (ext) {
+        ox = wred_max(live ? tx : -INFINITY);
+        on = wred_min(live ? tn : INFINITY);
+        oa = wred_max(live ? va : 0.f);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        float* q = red + wave * 8;
+        q[0] = wm;
+        q[1] = __int_as_float(idx);
+        q[2] = ws;
+        q[3] = ox;
+        q[4] = on;
+        q[5] = oa;
+    }
+}
+
+// Operator fragments a wave keeps in VGPRs across all rounds (REGOPS).
+// Capacities mirror regops_fit (irm_kernels.hpp): a 512-thread workgroup (8 waves) keeps 4 stage-1
+// k-quads and 2 stage-2 tiles per wave (N ≤ 128 at R = 32), a 256-thread one up to 8 of each.
+
+// Problem shape of an optimiser launch.  FixShape: compile-time N / R (and everything derived,
+// incl. the LDS layout head) for the common shapes; DynShape: any shape, read from KParams.
+template <int D_, int N_, int RP_>
+struct FixShape {
+    static constexpr int D = D_, N = N_, NK = (N_ + 15) / 16 * 16, MP = 2 * NK, RP = RP_;
+    static constexpr int NW = (N_ + 63) / 64 * 64, WPT = NW / 64, NSPLIT = stage1_splits(NK);
+    static constexpr bool kVariants = false;  // end-effector cost only (the reference's)
+    __device__ explicit FixShape(const KParams&) {}
+};
+template <int D_>
+struct DynShape {
+    static constexpr int D = D_;
+    static constexpr bool kVariants = true;  // cost variants chosen at run time (whole_robot)
+    int N, NK, MP, RP, NW, WPT, NSPLIT;
+    __device__ explicit DynShape(const KParams& P)
+        : N(P.N), NK(P.NK), MP(P.MP), RP(P.RP), NW(P.NW), WPT(P.NW >> 6), NSPLIT(P.nsplit) {}
+};
+constexpr int kS1Q(int maxt) { return maxt <= 256 ? 8 : 4; }   // stage-1 float4 per wave
+constexpr int kS2T(int maxt) { return maxt <= 256 ? 8 : 2; }   // stage-2 tiles per wave (KQ2 ≤ 2)
+
+// Row layout of the optimiser's [a; b] / [T; V] buffers and of F: the velocity
+// half starts at row NK (= N rounded up to 16), so the position half is whole
+// k-quads of its own and stage 1 can skip the velocity half when b is zero
+// away from the two endpoint rows (the usual case); the endpoint rows then enter
+// through the precomputed operator columns h0 = F·F[NK]ᵀ, h1 = F·F[NK+N−1]ᵀ.
+//
+// One round of a workgroup (TB trajectories, one lane per waypoint):
+//   stage 1   y' = Fᵀ·[a'; b']          (MFMA, split-K over the waves → Ypart)
+//             a' = a·JᵀJ, b' = b·JᵀJ were mixed per lane when written, so y' = y·JᵀJ
+//   stage 2   Δ[T; V] = F·y'            (MFMA; B operand = Σ partials, summed on load)
+//   update    [T; V]' = c·[T; V] − s·Δ  (Δ latched in registers per direction)
+//   evaluate  cost at the trial point; gradient inputs for the next direction
+//   decide    the reference's accept / reject / λ logic per trajectory
+// α is not carried: each lane accumulates the gradient inputs of the accepted
+// steps (acc = c·acc + s·[a'; b']), and α = cprod·α_base − V_R·Fᵀ·acc·J⁻¹ is
+// formed only when an inner loop ends (PH_RESYNC).
+template <class S, int MAXT, bool OPS_LDS, bool REGOPS, bool BLS>
+__global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
+    constexpr int D = S::D;
+    constexpr int S1Q = kS1Q(MAXT), S2T = kS2T(MAXT);
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const S sh(P);
+    const Head H = plan_head(sh.MP, sh.RP, sh.NSPLIT, true);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nwaves = P.BT >> 6;
+    const int N = sh.N, NW = sh.NW, TB = P.TB, RP = sh.RP, MP = sh.MP, NK = sh.NK;
+    const int WPT = sh.WPT;             // waves per trajectory
+    const int t = wave / WPT;           // this lane's trajectory (wave-uniform)
+    const int n = tid - t * NW;         // this lane's waypoint (and row r of y for n < RP)
+    const int n0 = (wave - t * WPT) * 64;  // first waypoint of this wave
+    const int tb0 = blockIdx.x * TB;
+    const int ntb = min(TB, P.B - tb0);
+    if (ntb <= 0) return;
+    const bool tvalid = t < ntb;
+    const bool valid = tvalid && n < N;
+    const bool yrow = tvalid && n < RP;
+    const size_t b = (size_t)(tb0 + (tvalid ? t : 0));
+    constexpr bool bls = BLS;
+    const bool rec = P.record_series && P.series;
+    Prof prof;
+    if (tid == 0) prof.init();
+
+    float* X = smem + H.X;    // [a'; b'] (rows 0..N-1, NK..NK+N-1) × 16 columns
+    float* dP = smem + H.dP;  // Δ[T; V], same row layout
+    float* Ypart = smem + H.Ypart;
+    float* Ymix = smem + H.Ymix;
+    float* red = smem + H.red;
+    float* sg = smem + H.sg;
+    float* wp = smem + H.wp;
+    // [0,1] direction masks (bit per column) and [3,4] resync masks (bit per trajectory) by
+    // round parity; [2] done mask; [5,6] "b' non-zero away from the endpoints" by round parity
+    unsigned* flagw = reinterpret_cast<unsigned*>(smem + H.flags);
+    float* obsL = smem + H.obs;
+    const float* F1 = P.F1frag;
+    const float* F2 = P.F2frag;
+
+    const int KQ1 = MP / 16, KQa = NK / 16, MT1 = RP / 16;  // stage 1: (RP × MP)·(MP × 16)
+    const int KQ2 = RP / 16, MT2 = MP / 16;                 // stage 2: (MP × RP)·(RP × 16)
+    const int nsplit = sh.NSPLIT;
+    // stage-1 unit of this wave (split-K over the position half): tile, k-quads [kq0, kq1)
+    const bool has1 = wave < MT1 * nsplit;
+    const int tile1 = wave % MT1, sp1 = wave / MT1;
+    const int kq0 = (KQa * sp1) / nsplit, kq1 = (KQa * (sp1 + 1)) / nsplit;
+
+    // ----------------------------------------------------------- prologue
+    if (OPS_LDS && !REGOPS) {
+        const Plan L = plan_lds(P, OPS_LDS, true);
+        const int n1 = (int)frag_floats(RP, MP) / 4, n2 = (int)frag_floats(MP, RP) / 4;
+        const f32x4* g1 = reinterpret_cast<const f32x4*>(P.F1frag);
+        const f32x4* g2 = reinterpret_cast<const f32x4*>(P.F2frag);
+        f32x4* l1 = reinterpret_cast<f32x4*>(smem + L.f1);
+        f32x4* l2 = reinterpret_cast<f32x4*>(smem + L.f2);
+        for (int e = tid; e < n1; e += P.BT) l1[e] = g1[e];
+        for (int e = tid; e < n2; e += P.BT) l2[e] = g2[e];
+        F1 = smem + L.f1;
+        F2 = smem + L.f2;
+    }
+    f32x4 a1[REGOPS ? S1Q : 1], a2[REGOPS ? S2T * 2 : 1];
+    if (REGOPS) {  // operator A-fragments resident in VGPRs for the whole launch
+        const f32x4* g1 = reinterpret_cast<const f32x4*>(P.F1frag);
+        const f32x4* g2 = reinterpret_cast<const f32x4*>(P.F2frag);
+#pragma unroll
+        for (int i = 0; i < S1Q; ++i) {
+            a1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (has1 && kq0 + i < kq1) a1[i] = g1[((size_t)tile1 * KQ1 + kq0 + i) * 64 + lane];
+        }
+#pragma unroll
+        for (int j = 0; j < S2T; ++j)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                a2[j * 2 + i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                const int tile = wave + j * nwaves;
+                if (tile < MT2 && i < KQ2) a2[j * 2 + i] = g2[((size_t)tile * KQ2 + i) * 64 + lane];
+            }
+    }
+    // endpoint-velocity operator columns for this lane's rows (sparse stage 1), and the
+    // F rows of the two endpoint velocities for the BLS norms (rows r = n < RP)
+    const float h0T = valid ? P.Hend[n] : 0.f, h1T = valid ? P.Hend[MP + n] : 0.f;
+    const float h0V = valid ? P.Hend[NK + n] : 0.f, h1V = valid ? P.Hend[MP + NK + n] : 0.f;
+    const float fb0 = yrow ? P.Fbot[(size_t)0 * RP + n] : 0.f;
+    const float fb1 = yrow ? P.Fbot[(size_t)(N - 1) * RP + n] : 0.f;
+    stage_obstacles(P, tb0, ntb, obsL);
+    for (int e = tid; e < RP * kLd; e += P.BT) Ymix[e] = 0.f;
+    if (tid < 8) flagw[tid] = 0u;
+    // Parameters used only on rare paths (outer-loop step, line search, resync, series) live in
+    // LDS so that they hold no SGPRs across the loop.
+    float* cold = smem + H.cold;
+    for (int i = tid; i < kColdWords; i += P.BT) {
+        float val = 0.f;
+        if (i < IRM_MAX_LR) val = P.gd_lr[i];
+        else if (i == C_LCI) val = P.lci;
+        else if (i == C_EPSP) val = P.eps_p;
+        else if (i == C_EPSV) val = P.eps_v;
+        else if (i == C_PMAX) val = P.pmax;
+        else if (i == C_PMIN) val = P.pmin;
+        else if (i == C_VMAX) val = P.vmax;
+        else if (i == C_BLR0) val = P.bls_lr0;
+        else if (i == C_BA) val = P.bls_a;
+        else if (i == C_BP) val = P.bls_bp;
+        else if (i == C_BM) val = P.bls_bm;
+        else if (i == C_MAXOUT) val = __int_as_float(P.max_outer);
+        else if (i == C_MAXBLS) val = __int_as_float(P.max_bls);
+        else if (i == C_MAXSER) val = __int_as_float(P.max_series);
+        else if (i >= C_PTR && i < C_PTR + 8) {
+            const int w = i - C_PTR;
+            const void* ptrs[4] = {P.series, P.Vr, P.Kt, P.dKt};
+            const uint64_t a = reinterpret_cast<uint64_t>(ptrs[w >> 1]);
+            val = __uint_as_float((w & 1) ? (uint32_t)(a >> 32) : (uint32_t)a);
+        } else if (i >= C_MINV && i < C_MINV + D * D) val = P.Minv[i - C_MINV];
+        else if (i >= C_WAL && i < C_WAL + D) val = P.wal[i - C_WAL];
+        else if (i >= C_JINV && i < C_JINV + D * D) val = P.Jinv[i - C_JINV];
+        cold[i] = val;
+    }
+    auto cold_ptr = [&](int w) -> float* {
+        const uint64_t lo = __float_as_uint(cold[C_PTR + 2 * w]), hi = __float_as_uint(cold[C_PTR + 2 * w + 1]);
+        return reinterpret_cast<float*>(lo | (hi << 32));
+    };
+    auto cold_int = [&](int i) { return __float_as_int(cold[i]); };
+    stage_alpha<D>(P, tb0, ntb, X, NK);
+    __syncthreads();
+    // T0 = (K·α0)·J, V0 = (dK·α0)·J  (trajectory.py:63-65), correctly rounded.
+    // ab: this lane's row of the α the state is expressed against (α0, then the α
+    // materialised at the last resync).
+    float q[D], v[D], s[D], g[D], ab[D], dT[D], dV[D], dra[D], drb[D], aca[D], acb[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        q[k] = v[k] = 0.f;
+        dT[k] = dV[k] = dra[k] = drb[k] = aca[k] = acb[k] = 0.f;
+        ab[k] = valid ? X[n * kLd + t * D + k] : 0.f;
+        s[k] = tvalid ? P.start[b * D + k] : 0.f;
+        g[k] = tvalid ? P.goal[b * D + k] : 0.f;
+    }
+    if (valid) {
+        eval_exact<D>(P, X + t * D, n, q, v);
+        if (rec) {
+#pragma unroll
+            for (int k = 0; k < D; ++k) P.series[(b * P.max_series) * N * D + n * D + k] = q[k];
+        }
+    }
+    __syncthreads();  // every lane has read α0 from X
+    for (int e = tid; e < MP * kLd; e += P.BT) X[e] = 0.f;
+    const float* obs = obsL + (P.obs_stride ? t * obs_pitch(P.O) : 0);
+
+    // stage 1 over the units of this wave: Ypart[s] = Fᵀ·[a'; b'] (velocity half if `full`)
+    auto stage1 = [&](bool full) {
+        const float* xl = X + (lane >> 4) * kLd + (lane & 15);
+        auto quads = [&](const f32x4* ap, int qoff, int k0, int k1, f32x4& acc0, f32x4& acc1) {
+            for (int kq = k0; kq < k1; ++kq) {
+                const f32x4 a = ap[(size_t)kq * 64];
+                const float* xb = xl + (qoff + kq) * 16 * kLd;
+                const float b0 = xb[0], b1 = xb[4 * kLd], b2 = xb[8 * kLd], b3 = xb[12 * kLd];
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b0, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b1, acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b2, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b3, acc1, 0, 0, 0);
+            }
+        };
+        if (REGOPS) {  // one unit per wave (regops_fit), position-half fragments in VGPRs
+            if (has1) {
+                float bv[S1Q][4];
+#pragma unroll
+                for (int i = 0; i < S1Q; ++i) {
+                    const float* xb = xl + (kq0 + i) * 16 * kLd;
+                    const bool in = kq0 + i < kq1;
+                    bv[i][0] = in ? xb[0] : 0.f;
+                    bv[i][1] = in ? xb[4 * kLd] : 0.f;
+                    bv[i][2] = in ? xb[8 * kLd] : 0.f;
+                    bv[i][3] = in ? xb[12 * kLd] : 0.f;
+                }
+                f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int i = 0; i < S1Q; ++i) {
+                    if (kq0 + i < kq1) {
+                        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][0], bv[i][0], acc0, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][1], bv[i][1], acc1, 0, 0, 0);
+                        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][2], bv[i][2], acc0, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][3], bv[i][3], acc1, 0, 0, 0);
+                    }
+                }
+                if (full)
+                    quads(reinterpret_cast<const f32x4*>(F1) + ((size_t)tile1 * KQ1 + KQa) * 64 + lane, KQa, kq0,
+                          kq1, acc0, acc1);
+                store_tile(Ypart + sp1 * RP * kLd, tile1, acc0 + acc1, 0xFFFFu);
+            }
+        } else {
+            for (int u = wave; u < MT1 * nsplit; u += nwaves) {
+                const int tile = u % MT1, sp = u / MT1;
+                const int k0 = (KQa * sp) / nsplit, k1 = (KQa * (sp + 1)) / nsplit;
+                f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+                const f32x4* ap = reinterpret_cast<const f32x4*>(F1) + ((size_t)tile * KQ1) * 64 + lane;
+                quads(ap, 0, k0, k1, acc0, acc1);
+                if (full) quads(ap + (size_t)KQa * 64, KQa, k0, k1, acc0, acc1);
+                store_tile(Ypart + sp * RP * kLd, tile, acc0 + acc1, 0xFFFFu);
+            }
+        }
+    };
+
+    // replicated per-trajectory scalar state
+    float loss = 0.f, lsg = P.lsg0, ljl = P.ljl0, lr = 0.f, cprod = 1.f, gnorm = 1.f, anorm = 0.f;
+    float cfac = 1.f, step = 0.f;
+    int phase = tvalid ? PH_OUTER_START : PH_DONE, outer = 0, inner = 0, trial = 0;
+    bool needs_dir = false;
+    irm_stats st{};
+    st.series_len = rec ? 1 : 0;
+    const unsigned tmask = (1u << D) - 1u;
+    const unsigned fullmask = (ntb >= 32) ? 0xFFFFFFFFu : ((1u << ntb) - 1u);
+    __syncthreads();
+    IRM_STAMP(14);
+
+    for (int round = 0;; ++round) {
+        const int par = round & 1;
+        const unsigned dirmask = flagw[par];
+        const unsigned rmask = flagw[3 + par];
+        const bool dense = flagw[5 + par] != 0u;  // b' has rows beyond the endpoints: full stage 1
+        IRM_STAMP(4);
+        if (tid == 0) {  // next round's masks (set in this round's flag section)
+            flagw[par ^ 1] = 0u;
+            flagw[3 + (par ^ 1)] = 0u;
+            flagw[5 + (par ^ 1)] = 0u;
+        }
+        // ------------------------------------------------ direction (stage 1+2)
+        if (dirmask) {
+            // the direction's gradient inputs: this lane's rows (α recovery) and the two
+            // endpoint velocity rows of its trajectory (sparse stage 1)
+            float e0[D], e1[D];
+            if (needs_dir) {
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    dra[k] = valid ? X[n * kLd + t * D + k] : 0.f;
+                    drb[k] = valid ? X[(NK + n) * kLd + t * D + k] : 0.f;
+                    e0[k] = X[NK * kLd + t * D + k];
+                    e1[k] = X[(NK + N - 1) * kLd + t * D + k];
+                }
+            }
+            stage1(dense);
+            IRM_STAMP(5);
+            __syncthreads();
+            IRM_STAMP(0);
+            // BLS norms from y' rows (lane n = row r):
+            //   ‖G‖² = Σ_r y'(JᵀJ)⁻¹y'ᵀ,  alpha_norm·‖G‖ = Σ_r (y'·w)², w = (JᵀJ)⁻¹Jᵀ1
+            if (bls && needs_dir) {
+                float g2 = 0.f, al = 0.f;
+                if (yrow) {
+                    float y[D];
+#pragma unroll
+                    for (int d = 0; d < D; ++d) y[d] = dense ? 0.f : fmaf(fb0, e0[d], fb1 * e1[d]);
+                    for (int sp = 0; sp < nsplit; ++sp) {
+#pragma unroll
+                        for (int d = 0; d < D; ++d) y[d] += Ypart[(sp * RP + n) * kLd + t * D + d];
+                    }
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        float m = 0.f;
+#pragma unroll
+                        for (int d = 0; d < D; ++d) m += y[d] * cold[C_MINV + d * D + k];
+                        g2 += y[k] * m;
+                        al += cold[C_WAL + k] * y[k];
+                    }
+                    al = al * al;
+                }
+                g2 = wred_sum(g2);
+                al = wred_sum(al);
+                if (lane == 0) {
+                    wp[wave * 2] = g2;
+                    wp[wave * 2 + 1] = al;
+                }
+            }
+            IRM_STAMP(2);
+            // stage 2: dP = F(MP × RP)·Σ_s Ypart[s], only the direction columns
+            {
+                const float* xl = Ypart + (lane >> 4) * kLd + (lane & 15);
+                auto bload = [&](int i, float& b0, float& b1, float& b2, float& b3) {
+                    b0 = b1 = b2 = b3 = 0.f;
+                    for (int sp = 0; sp < nsplit; ++sp) {
+                        const float* xb = xl + (sp * RP + i * 16) * kLd;
+                        b0 += xb[0];
+                        b1 += xb[4 * kLd];
+                        b2 += xb[8 * kLd];
+                        b3 += xb[12 * kLd];
+                    }
+                };
+                if (REGOPS) {
+                    f32x4 acc[S2T];
+#pragma unroll
+                    for (int j = 0; j < S2T; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    float bv[2][4];
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        if (i < KQ2) bload(i, bv[i][0], bv[i][1], bv[i][2], bv[i][3]);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        if (i < KQ2) {
+#pragma unroll
+                            for (int j = 0; j < S2T; ++j) {
+                                if (wave + j * nwaves < MT2) {
+                                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][0], bv[i][0], acc[j], 0, 0, 0);
+                                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][1], bv[i][1], acc[j], 0, 0, 0);
+                                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][2], bv[i][2], acc[j], 0, 0, 0);
+                                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][3], bv[i][3], acc[j], 0, 0, 0);
+                                }
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int j = 0; j < S2T; ++j)
+                        if (wave + j * nwaves < MT2) store_tile(dP, wave + j * nwaves, acc[j], dirmask);
+                } else {
+                    for (int tile = wave; tile < MT2; tile += nwaves) {
+                        f32x4 c0 = {0.f, 0.f, 0.f, 0.f};
+                        const f32x4* ap = reinterpret_cast<const f32x4*>(F2) + ((size_t)tile * KQ2) * 64 + lane;
+                        for (int i = 0; i < KQ2; ++i) {
+                            float b0, b1, b2, b3;
+                            bload(i, b0, b1, b2, b3);
+                            const f32x4 a = ap[(size_t)i * 64];
+                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b0, c0, 0, 0, 0);
+                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b1, c0, 0, 0, 0);
+                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b2, c0, 0, 0, 0);
+                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b3, c0, 0, 0, 0);
+                        }
+                        store_tile(dP, tile, c0, dirmask);
+                    }
+                }
+            }
+            __syncthreads();
+            IRM_STAMP(3);
+            if (needs_dir) {
+                // latch this lane's direction rows (+ the endpoint-velocity columns)
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    float ut = dP[n * kLd + t * D + k], uv = dP[(NK + n) * kLd + t * D + k];
+                    if (!dense) {
+                        ut = fmaf(h0T, e0[k], fmaf(h1T, e1[k], ut));
+                        uv = fmaf(h0V, e0[k], fmaf(h1V, e1[k], uv));
+                    }
+                    dT[k] = ut;
+                    dV[k] = uv;
+                }
+                if (bls) {
+                    float tg = 0.f, ta = 0.f;
+                    for (int ww = 0; ww < WPT; ++ww) {
+                        tg += wp[(t * WPT + ww) * 2];
+                        ta += wp[(t * WPT + ww) * 2 + 1];
+                    }
+                    gnorm = sqrtf(tg);
+                    anorm = ta / gnorm;
+                    st.grad_evals++;  // inner-loop head: cost + grad at α (optimizer_BLS.py:163-164)
+                    st.cost_evals++;
+                    phase = PH_BLS_TRIAL;
+                    trial = 0;
+                } else {
+                    cfac = 1.f - P.lreg * lr;
+                    step = lr;
+                }
+                needs_dir = false;
+            }
+        }
+        if (phase == PH_BLS_TRIAL) {
+            cfac = 1.f - P.lreg * lr;
+            step = lr / gnorm;
+        }
+        // ------------------------------------------------------- resync
+        // Trajectories whose inner loop ended last round: α = cprod·ab −
+        // V_R·(Fᵀ·acc)·J⁻¹ in fp32 (what the reference carries), then [T; V] =
+        // eval_exact(α), so the constraint check below and the caller's
+        // evaluate(α_out) see the same waypoints bit for bit.
+        if (rmask) {  // block-uniform
+            const bool rs = tvalid && ((rmask >> t) & 1u);  // wave-uniform
+            if (rs && valid) {
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    X[n * kLd + t * D + k] = aca[k];
+                    X[(NK + n) * kLd + t * D + k] = acb[k];
+                }
+            }
+            __syncthreads();
+            stage1(true);
+            __syncthreads();
+            if (rs && yrow) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    float y = 0.f;
+                    for (int sp = 0; sp < nsplit; ++sp) y += Ypart[(sp * RP + n) * kLd + t * D + d];
+                    Ymix[n * kLd + t * D + d] = y;
+                }
+            }
+            __syncthreads();
+            if (rs && valid) {
+                float z[D];
+#pragma unroll
+                for (int l = 0; l < D; ++l) z[l] = 0.f;
+                const float* vr = cold_ptr(1) + (size_t)n * RP;
+                for (int r = 0; r < RP; ++r) {
+                    const float vv = vr[r];
+#pragma unroll
+                    for (int l = 0; l < D; ++l) z[l] += vv * Ymix[r * kLd + t * D + l];
+                }
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int l = 0; l < D; ++l) acc += z[l] * cold[C_JINV + l * D + k];
+                    ab[k] = cprod * ab[k] - acc;
+                    X[n * kLd + t * D + k] = ab[k];
+                }
+            }
+            __syncthreads();
+            if (rs) {
+                if (valid) {
+                    eval_exact<D>(P, X + t * D, n, q, v, cold_ptr(2), cold_ptr(3));
+                    // the last extended-vis frame shows the materialised α's trajectory
+                    if (rec && st.series_len > 0) {
+                        float* ser = cold_ptr(0);
+                        const int ms = cold_int(C_MAXSER);
+#pragma unroll
+                        for (int k = 0; k < D; ++k) ser[((b * ms) + st.series_len - 1) * N * D + n * D + k] = q[k];
+                    }
+                }
+                cprod = 1.f;
+#pragma unroll
+                for (int k = 0; k < D; ++k) aca[k] = acb[k] = 0.f;
+            }
+        }
+        // ------------------------------------------------------- update
+        float q2[D], v2[D];
+        if (phase == PH_GD_INNER || phase == PH_BLS_TRIAL) {
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                q2[k] = cfac * q[k] - step * dT[k];
+                v2[k] = cfac * v[k] - step * dV[k];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                q2[k] = q[k];
+                v2[k] = v[k];
+            }
+        }
+        // ------------------------------------------------------- evaluate
+        IRM_STAMP(6);
+        const bool ev = (phase != PH_DONE);  // wave-uniform
+        WP<D> w;
+        if (ev) {
+            if (valid) {
+                if constexpr (S::kVariants) eval_waypoint_rt<D>(P, q2, v2, obs, w);
+                else eval_waypoint<D>(P, q2, v2, obs, w);
+            }
+            IRM_STAMP(8);
+            const float us = P.one_m_lmax * (w.cv * P.invN) + ljl * ((w.jp + w.jv) * P.invN);
+            ered_store(valid, w.cv, us, w.tx, w.tn, w.va, phase == PH_RESYNC, n0, red, wave);
+            if (valid && (n == 0 || n == N - 1)) {  // trajectory.py:183-204 rows 0 and N−1
+                float a = 0.f, bb = 0.f;
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    const float e = q2[d] - (n == 0 ? s[d] : g[d]);
+                    a += e * e;
+                    bb += v2[d] * v2[d];
+                }
+                sg[t * 4 + (n == 0 ? 0 : 2)] = a;
+                sg[t * 4 + (n == 0 ? 1 : 3)] = bb;
+            }
+        }
+        IRM_STAMP(9);
+        __syncthreads();
+        IRM_STAMP(7);
+        if (ev) {
+            // combine the trajectory's wave partials (fixed order)
+            const float* r0 = red + (t * WPT) * 8;
+            float cmax = r0[0];
+            int cidx = __float_as_int(r0[1]);
+            float usum = r0[2], tx = r0[3], tn = r0[4], va = r0[5];
+            for (int ww = 1; ww < WPT; ++ww) {
+                const float* rw = red + (t * WPT + ww) * 8;
+                amax_step(cmax, cidx, rw[0], __float_as_int(rw[1]));
+                usum += rw[2];
+                tx = fmaxf(tx, rw[3]);
+                tn = fminf(tn, rw[4]);
+                va = fmaxf(va, rw[5]);
+            }
+            const float e_a0 = sg[t * 4 + 0], e_b0 = sg[t * 4 + 1], e_a1 = sg[t * 4 + 2], e_b1 = sg[t * 4 + 3];
+            const float sgpc = 0.5f * e_a0 + 0.5f * e_a1;                       // trajectory.py:187
+            const float sgvc = 0.5f * e_b0 + 0.5f * e_b1;                       // trajectory.py:203
+            // trajectory.py:85-87 + 281 (mean and joint-limit terms pre-summed in usum)
+            const float nl = (P.lam_max * cmax + usum) + lsg * (sgpc + sgvc);
+            const float lsg_e = lsg, ljl_e = ljl;
+            // --------------------------------------------------- decide
+            int accept = 0;
+            bool snap = false, to_end = false;
+            if (phase == PH_OUTER_START) {  // optimizer_GD.py:422-424 / optimizer_BLS.py:193
+                loss = nl;
+                if (!bls) st.cost_evals++;
+                accept = 2;
+                lr = bls ? cold[C_BLR0] : cold[outer];
+                needs_dir = true;
+                if (!bls) phase = PH_GD_INNER;
+                if (P.max_inner <= 0) to_end = true;
+            } else if (phase == PH_BLS_REEVAL) {  // gradient at the unchanged α after a fully rejected search
+                needs_dir = true;
+            } else if (phase == PH_RESYNC) {
+                // constraintsFulfilled(α) (trajectory.py:129-137, robot.py:90-113) on the
+                // materialised α; optimizer_GD.py:427-437 / optimizer_BLS.py:201-211
+                const float eps_p = cold[C_EPSP], eps_v = cold[C_EPSV];
+                const bool ok = sqrtf(e_a0) < eps_p && sqrtf(e_a1) < eps_p && sqrtf(e_b0) < eps_v &&
+                                sqrtf(e_b1) < eps_v && tx <= cold[C_PMAX] && tn >= cold[C_PMIN] && va <= cold[C_VMAX];
+                st.outer_iterations++;
+                st.constraints_ok = ok ? 1 : 0;
+                if (ok) {
+                    phase = PH_DONE;
+                } else {
+                    outer++;
+                    lsg = lsg * cold[C_LCI];
+                    ljl = ljl * cold[C_LCI];
+                    inner = 0;
+                    phase = (outer >= cold_int(C_MAXOUT)) ? PH_DONE : PH_OUTER_START;
+                }
+            } else if (phase == PH_GD_INNER) {  // optimizer_GD.py:394-408
+                st.grad_evals++;
+                st.cost_evals++;
+                if (loss - nl < P.llr) {
+                    to_end = true;  // minimized: the step is discarded
+                } else {
+                    accept = 1;
+                    loss = nl;
+                    inner++;
+                    st.inner_iterations++;
+                    snap = true;
+                    if (inner >= P.max_inner) to_end = true;
+                    else needs_dir = true;
+                }
+            } else {  // PH_BLS_TRIAL: optimizer_BLS.py:136-150, 172-178
+                st.cost_evals++;
+                st.bls_trials++;
+                const float required = loss - cold[C_BA] * lr * anorm;
+                bool inner_end = false, rejected_all = false;
+                float improve = 0.f;
+                if (nl > required) {
+                    lr = lr * cold[C_BM];
+                    trial++;
+                    if (trial >= cold_int(C_MAXBLS)) inner_end = rejected_all = true;  // new_loss = loss
+                } else {
+                    accept = 1;
+                    lr = lr * cold[C_BP];
+                    improve = loss - nl;
+                    loss = nl;
+                    inner_end = true;
+                }
+                if (inner_end) {
+                    if (improve < P.llr) {
+                        to_end = true;
+                    } else {
+                        inner++;
+                        st.inner_iterations++;
+                        snap = true;
+                        if (inner >= P.max_inner) to_end = true;
+                        else if (rejected_all) phase = PH_BLS_REEVAL;
+                        else needs_dir = true;
+                    }
+                }
+            }
+            if (to_end) {  // inner loop over: materialise α next round, then check constraints
+                st.final_loss = loss;
+                needs_dir = false;
+                phase = PH_RESYNC;
+            }
+            IRM_STAMP(10);
+            // ------------------------- gradient inputs at T2, mixed by JᵀJ (→ y' = y·JᵀJ)
+            bool bfar = false;
+            if (valid) {
+                float a[D], bb[D];
+                grad_waypoint<D>(P, w, q2, v2, n, cidx, lsg_e, ljl_e, s, g, a, bb);
+                const bool endrow = (n == 0 || n == N - 1);
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    float ma = 0.f, mb = 0.f;
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        ma += a[d] * P.JtJ[d * D + k];
+                        mb += bb[d] * P.JtJ[d * D + k];
+                    }
+                    X[n * kLd + t * D + k] = ma;
+                    X[(NK + n) * kLd + t * D + k] = mb;
+                    bfar |= (!endrow && bb[k] != 0.f);
+                }
+            }
+            if (__ballot(bfar) && lane == 0) atomicOr(&flagw[5 + (par ^ 1)], 1u);
+            IRM_STAMP(12);
+            // --------------------------------------------------- accept
+            if (accept == 1) {
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    q[k] = q2[k];
+                    v[k] = v2[k];
+                    aca[k] = cfac * aca[k] + step * dra[k];  // α recovery: Σ steps·[a'; b']
+                    acb[k] = cfac * acb[k] + step * drb[k];
+                }
+                cprod *= cfac;
+            }
+            // extended-vis snapshot after every non-breaking inner iteration
+            // (optimizer_GD.py:366-367, optimizer_BLS.py:106-107)
+            if (rec && snap && st.series_len < cold_int(C_MAXSER)) {
+                if (valid) {
+                    float* ser = cold_ptr(0);
+                    const int ms = cold_int(C_MAXSER);
+#pragma unroll
+                    for (int k = 0; k < D; ++k) ser[((b * ms) + st.series_len) * N * D + n * D + k] = q[k];
+                }
+                st.series_len++;
+            }
+            if (n == 0) {
+                if (needs_dir) atomicOr(&flagw[par ^ 1], tmask << (t * D));
+                if (phase == PH_DONE) atomicOr(&flagw[2], 1u << t);
+                if (phase == PH_RESYNC) atomicOr(&flagw[3 + (par ^ 1)], 1u << t);
+            }
+        }
+        IRM_STAMP(15);
+        __syncthreads();
+        IRM_STAMP(11);
+        if (flagw[2] == fullmask) break;
+    }
+
+    // ----------------------------------------------------------- epilogue
+    // Every trajectory ended through PH_RESYNC: acc = 0, cprod = 1, α = ab and
+    // T = eval_exact(α) exactly.
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            if (P.traj_out) P.traj_out[(b * N + n) * D + k] = q[k];
+            if (P.alpha_out) P.alpha_out[(b * N + n) * D + k] = ab[k];
+        }
+    }
+    if (P.stats && tvalid && n == 0) P.stats[b] = st;
+    IRM_STAMP(13);
+    if (tid == 0) prof.flush(P.prof);
+}
+
+// --------------------------------------------------- α-space eval kernels
+// mode 0: evaluate (K or dK)·α·J; 1: cost; 2: cost + grad; 3: constraints.
+// trajectory.py:63-65, 271-297, 129-180; same lane mapping as k_optimize.
+template <int D, int MAXT>
+__global__ __launch_bounds__(MAXT) void k_forward(KParams P, int mode) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const Plan L = plan_lds(P, false, false);
+    const int tid = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int N = P.N, NW = P.NW, TB = P.TB, MP = P.MP;
+    const int WPT = NW >> 6;
+    const int t = wave / WPT;
+    const int n = tid - t * NW;
+    const int tb0 = blockIdx.x * TB;
+    const int ntb = min(TB, P.B - tb0);
+    if (ntb <= 0) return;
+    const bool tvalid = t < ntb;
+    const bool valid = tvalid && n < N;
+    const size_t b = (size_t)(tb0 + (tvalid ? t : 0));
+    float* XG = smem + L.X;
+    float* red = smem + L.red;
+    float* sg = smem + L.sg;
+    float* obsL = smem + L.obs;
+
+    stage_obstacles(P, tb0, ntb, obsL);
+    stage_alpha<D>(P, tb0, ntb, XG, MP);
+    __syncthreads();
+    float q[D], v[D], s[D], g[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        q[k] = v[k] = 0.f;
+        s[k] = tvalid ? P.start[b * D + k] : 0.f;
+        g[k] = tvalid ? P.goal[b * D + k] : 0.f;
+    }
+    if (valid) eval_exact<D>(P, XG + t * D, n, q, v);
+    __syncthreads();
+    if (mode == 0) {
+        if (valid) {
+#pragma unroll
+            for (int k = 0; k < D; ++k) P.out0[(b * N + n) * D + k] = P.which ? v[k] : q[k];
+        }
+        return;
+    }
+    WP<D> w;
+    if (tvalid) {
+        if (valid) eval_waypoint_rt<D>(P, q, v, obsL, w);
+        eval_partials<D>(P, valid, w, n, wave, q, v, s, g, red, sg, t);
+    }
+    __syncthreads();
+    EvalOut E{};
+    if (tvalid) E = eval_finalize(P, red, sg, t, t * WPT, WPT, P.lam_sg, P.lam_jl);
+    if (tvalid && n == 0) {
+        if (mode == 1 || mode == 2) {
+            if (P.out0) P.out0[b] = E.loss;
+        } else if (mode == 3) {
+            const bool f0 = E.ds < P.eps_p && E.dg < P.eps_p;
+            const bool f1 = E.vs < P.eps_v && E.vg < P.eps_v;
+            const bool f2 = E.tmax <= P.pmax && E.tmin >= P.pmin;
+            const bool f3 = E.vabs <= P.vmax;
+            if (P.out_ok) P.out_ok[b] = (f0 && f1 && f2 && f3) ? 1 : 0;
+            if (P.out0) {
+                float* r = P.out0 + b * 11;
+                r[0] = E.ds; r[1] = E.dg; r[2] = E.vs; r[3] = E.vg;
+                r[4] = E.tmax; r[5] = E.tmin; r[6] = E.vabs;
+                r[7] = f0; r[8] = f1; r[9] = f2; r[10] = f3;
+            }
+        }
+    }
+    if (mode != 2) return;
+    if (valid) {
+        float a[D], bb[D];
+        grad_waypoint<D>(P, w, q, v, n, E.idx, P.lam_sg, P.lam_jl, s, g, a, bb);
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            XG[n * kLd + t * D + k] = a[k];
+            XG[(N + n) * kLd + t * D + k] = bb[k];
+        }
+    }
+    __syncthreads();
+    // G = (Kᵀa + dKᵀb)·Jᵀ  (trajectory.py:295)
+    if (valid) {
+        float G[D];
+        grad_exact<D>(P, XG + t * D, n, G);
+#pragma unroll
+        for (int k = 0; k < D; ++k) P.out1[(b * N + n) * D + k] = G[k];
+    }
+}
+
+// ------------------------------------------------------------- launchers
+template <class Fn>
+inline hipError_t dispatch_d(int D, Fn&& fn) {
+    switch (D) {
+        case 1: return fn(std::integral_constant<int, 1>{});
+        case 2: return fn(std::integral_constant<int, 2>{});
+        case 3: return fn(std::integral_constant<int, 3>{});
+        case 4: return fn(std::integral_constant<int, 4>{});
+        case 5: return fn(std::integral_constant<int, 5>{});
+        case 6: return fn(std::integral_constant<int, 6>{});
+        case 7: return fn(std::integral_constant<int, 7>{});
+        case 8: return fn(std::integral_constant<int, 8>{});
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <class Fn>
+inline hipError_t dispatch_t(int BT, Fn&& fn) {
+    if (BT <= 256) return fn(std::integral_constant<int, 256>{});
+    if (BT <= 512) return fn(std::integral_constant<int, 512>{});
+    if (BT <= 1024) return fn(std::integral_constant<int, 1024>{});
+    return hipErrorInvalidValue;
+}
+
+template <class K, class... Args>
+inline hipError_t launch_lds(K kernel, int grid, int threads, size_t lds, hipStream_t s, Args... args) {
+    hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kernel, dim3(grid), dim3(threads), lds, s, args...);
+    return hipGetLastError();
+}
+
+template <class T>
+struct type_tag {
+    using type = T;
+};
+
+// k_optimize<Shape> with the MAXT / operator-placement / optimiser variants (one shape per
+// instantiation unit, irm_opt_inst.hip).
+template <class Sh>
+hipError_t launch_optimize_shape(const KParams& p, hipStream_t s) {
+    const bool stage = p.ops_in_lds != 0;
+    const Plan L = plan_lds(p, stage, true);
+    const size_t lds = (size_t)L.total * 4;
+    const int grid = (p.B + p.TB - 1) / p.TB;
+    if (grid <= 0) return hipSuccess;
+    return dispatch_t(p.BT, [&](auto tc) {
+        constexpr int TT = decltype(tc)::value;
+        auto go = [&](auto bc) {
+            constexpr bool BB = decltype(bc)::value;
+            if constexpr (TT <= 512) {
+                if (p.regops) return launch_lds(k_optimize<Sh, TT, true, true, BB>, grid, p.BT, lds, s, p);
+            }
+            return stage ? launch_lds(k_optimize<Sh, TT, true, false, BB>, grid, p.BT, lds, s, p)
+                         : launch_lds(k_optimize<Sh, TT, false, false, BB>, grid, p.BT, lds, s, p);
+        };
+        return p.optimizer == IRM_OPT_BLS ? go(std::integral_constant<bool, true>{})
+                                          : go(std::integral_constant<bool, false>{});
+    });
+}
+
+template <int D>
+hipError_t launch_forward_dim(const KParams& p, int mode, hipStream_t s) {
+    const Plan L = plan_lds(p, false, false);
+    const size_t lds = (size_t)L.total * 4;
+    const int grid = (p.B + p.TB - 1) / p.TB;
+    if (grid <= 0) return hipSuccess;
+    return dispatch_t(p.BT, [&](auto tc) {
+        constexpr int TT = decltype(tc)::value;
+        return launch_lds(k_forward<D, TT>, grid, p.BT, lds, s, p, mode);
+    });
+}
+
+// Instantiated in irm_opt_inst.hip (IRM_INST_* macros); irm_kernels.hip only dispatches.
+#define IRM_FIX_SHAPES(X) X(3, 50) X(3, 64) X(3, 128) X(3, 256) X(7, 256)
+#define IRM_EXTERN_FIX(D_, N_) extern template hipError_t launch_optimize_shape<FixShape<D_, N_, 32>>(const KParams&, hipStream_t);
+#define IRM_EXTERN_DYN(D_)                                                                          \
+    extern template hipError_t launch_optimize_shape<DynShape<D_>>(const KParams&, hipStream_t); \
+    extern template hipError_t launch_forward_dim<D_>(const KParams&, int, hipStream_t);
+
+}  // namespace irm
