@@ -610,7 +610,7 @@ constexpr int kS2T(int maxt) { return maxt <= 256 ? 8 : 2; }   // stage-2 tiles 
 // steps (acc = c·acc + s·[a'; b']), and α = cprod·α_base − V_R·Fᵀ·acc·J⁻¹ is
 // formed only when an inner loop ends (PH_RESYNC).
 template <class S, int MAXT, bool OPS_LDS, bool REGOPS, bool BLS>
-__global__ __launch_bounds__(MAXT) void k_optimize(KParams P) {
+__global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_optimize(KParams P) {
     constexpr int D = S::D;
     constexpr int S1Q = kS1Q(MAXT), S2T = kS2T(MAXT);
     extern __shared__ __attribute__((aligned(16))) float smem[];

@@ -10,11 +10,12 @@ Additive flags (no reference counterpart): --batch-size, --seed,
 --operator-rank, --device, --whole-robot-cost.
 """
 import argparse
+import os
 import time
 
 import numpy as np
 
-from . import batch_io
+from . import batch_io, distributed
 from .optimizer_BLS import BacktrackingLineSearchOptimizer
 from .optimizer_GD import GradientDescentOptimizer
 
@@ -120,25 +121,55 @@ def run_batch(optimizer, args):
 
     Timing lines as main.py:118-128 (one "took" per measurement, for the whole batch); the
     reference's report and files for problem 0 (the reference environment); batch files
-    and a one-line batch summary (batch_io.py)."""
+    and a one-line batch summary (batch_io.py).
+
+    Under torchrun (WORLD_SIZE > 1, one process per GPU) the batch is sharded:
+    rank 0's environment and problems are broadcast, every rank optimises its rows
+    [lo, hi), the results are all-gathered and rank 0 reports and writes the files."""
     env, tr = optimizer.env, optimizer.trajectory
-    start, goal = batch_io.batch_problems(args.batch_size, tr.robot.N_joints, args.seed)
+    world, rank, _ = distributed.world_info()
+    B = args.batch_size
+    start, goal = batch_io.batch_problems(B, tr.robot.N_joints, args.seed)
+    lo, hi = 0, B
+    dev = "cpu"
+    if world > 1:
+        import torch
+        dev = torch.device("cuda", args.device) if torch.distributed.get_backend() == "nccl" else "cpu"
+        obs, start, goal = distributed.broadcast_environment(env.obstacles, start, goal, dev)
+        env.obstacles = obs
+        lo, hi = distributed.shard(B, world, rank)
     runtimes = []
     res = None
     for _ in range(args.n_measurements):
         st = time.time()
         for _ in range(args.n_times):
-            res = optimizer.optimize_batch(start, goal, env.obstacles, series=args.extended_vis)
+            res = optimizer.optimize_batch(start[lo:hi], goal[lo:hi], env.obstacles, series=args.extended_vis)
         et = time.time()
+        if world > 1:
+            et = st + distributed.reduce_timing(et - st, 0, dev)[0]
         runtimes.append(1000 * (et - st) / args.n_times)
-        print("took", 1000 * (et - st) / args.n_times, "ms")
-    if args.n_measurements > 1:
+        if rank == 0:
+            print("took", 1000 * (et - st) / args.n_times, "ms")
+    if args.n_measurements > 1 and rank == 0:
         print("runtimes in ms: mean", np.mean(runtimes), "stddev", np.std(runtimes))
     alpha, traj, stats = res[:3]
+    series = res[3] if args.extended_vis else None
+    if world > 1:
+        parts = {"alpha": alpha, "traj": traj}
+        parts.update({"stat_" + k: np.asarray(v) for k, v in stats.items()})
+        if series is not None:
+            parts["series"] = series
+        full = distributed.gather_batch(parts, B, dev)
+        alpha, traj = full["alpha"], full["traj"]
+        stats = {k[5:]: v for k, v in full.items() if k.startswith("stat_")}
+        series = full.get("series")
+        if rank != 0:
+            return alpha
     avg = tr.compute_trajectory_cost(alpha, env.obstacles, start, goal, 0, 0, 0)
     mx = tr.compute_trajectory_cost(alpha, env.obstacles, start, goal, 0, 0, 1)
     ok, _ = optimizer.context.constraints(alpha, start, goal)
-    print("batch of", len(alpha), "problems: constraint fulfiled", int(np.sum(ok)), "of", len(alpha),
+    print("batch of", len(alpha), "problems" + (f" on {world} GPUs" if world > 1 else "") +
+          ": constraint fulfiled", int(np.sum(ok)), "of", len(alpha),
           "; avg cost mean", float(np.mean(avg)), ", max cost mean", float(np.mean(mx)),
           "; inner iterations", int(np.sum(stats["inner_iterations"])))
     ok0 = tr.constraintsFulfilledVerbose(alpha[0], start[0], goal[0], verbose=True)
@@ -146,8 +177,7 @@ def run_batch(optimizer, args):
     batch_io.write_result(batch_io.RESULT, traj[0])
     batch_io.write_result_batch(batch_io.RESULT_BATCH, traj)
     batch_io.write_summary(batch_io.SUMMARY_BATCH, avg, mx, ok, stats)
-    if args.extended_vis:
-        series = res[3]
+    if series is not None:
         lens = stats["series_len"]
         frames0 = series[0][: int(lens[0])]
         print(frames0.shape)
@@ -158,6 +188,20 @@ def run_batch(optimizer, args):
 
 def main(argv=None):
     args = parse_args(argv)
+    world, _, local = distributed.world_info()
+    if world > 1:  # torchrun: one process per GPU
+        import torch
+        import torch.distributed as dist
+        # IRM_DIST_BACKEND=gloo: host-side collectives (e.g. several ranks sharing one GPU in tests)
+        backend = os.environ.get("IRM_DIST_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
+        ngpu = torch.cuda.device_count()
+        args.device = local % max(1, ngpu)
+        if not dist.is_initialized():
+            if backend == "nccl":
+                torch.cuda.set_device(args.device)
+                dist.init_process_group("nccl", device_id=torch.device("cuda", args.device))
+            else:
+                dist.init_process_group("gloo")
     if args.optimizer_name == 'bls':
         optimizer = BacktrackingLineSearchOptimizer(args)
     elif args.optimizer_name == 'gd':

@@ -78,3 +78,60 @@ def test_two_rank_gloo_sharding(tmp_path):
         alpha, _ = orc.optimize_batch(None, s, g, obstacles, n_threads=1)
         np.testing.assert_array_equal(alpha, r[rank]["alpha"])
     assert len(full_start) == B
+
+
+def _gather_worker(rank, world, port, out_dir):
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch.distributed as dist
+
+    from irm_motion_planning_amd import distributed as D
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    B = 7  # uneven shards: 4 + 3
+    rng = np.random.default_rng(rank)  # every rank starts from different values ...
+    obs = rng.uniform(-3, 3, (11, 2)).astype(np.float32)
+    s = rng.uniform(-0.5, 0.5, (B, 3)).astype(np.float32)
+    g = rng.uniform(0.2, 1.6, (B, 3)).astype(np.float32)
+    obs, s, g = D.broadcast_environment(obs, s, g)  # ... and ends with rank 0's
+    lo, hi = D.shard(B, world, rank)
+    traj = np.repeat(s[lo:hi, None, :], 5, axis=1) * np.float32(2)  # a per-problem result
+    iters = np.arange(lo, hi, dtype=np.int64) * 10
+    ok = (np.arange(lo, hi) % 2).astype(np.uint8)
+    full = D.gather_batch({"traj": traj, "iters": iters, "ok": ok}, B)
+    t_max, it_sum = D.reduce_timing(0.5 * (rank + 1), hi - lo)
+    np.savez(os.path.join(out_dir, f"g{rank}.npz"), obs=obs, s=s, lo=lo, hi=hi, t_max=t_max, it_sum=it_sum,
+             **full)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_distributed_helpers_two_ranks(tmp_path):
+    """irm_motion_planning_amd.distributed over gloo, world 2: broadcast of rank 0's environment,
+    contiguous uneven shards, all-gather of float/int/uint8 per-problem results in rank order,
+    max/sum timing reduction (the nccl path of main.py --batch-size under torchrun)."""
+    world = 2
+    mp.start_processes(_gather_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    r = [dict(np.load(tmp_path / f"g{i}.npz")) for i in range(world)]
+    rng0 = np.random.default_rng(0)
+    obs0 = rng0.uniform(-3, 3, (11, 2)).astype(np.float32)
+    s0 = rng0.uniform(-0.5, 0.5, (7, 3)).astype(np.float32)
+    assert [(int(x["lo"]), int(x["hi"])) for x in r] == [(0, 4), (4, 7)]
+    for x in r:
+        np.testing.assert_array_equal(x["obs"], obs0)
+        np.testing.assert_array_equal(x["s"], s0)
+        np.testing.assert_array_equal(x["traj"], np.repeat(s0[:, None, :], 5, axis=1) * np.float32(2))
+        np.testing.assert_array_equal(x["iters"], np.arange(7) * 10)
+        assert x["iters"].dtype == np.int64 and x["ok"].dtype == np.uint8
+        np.testing.assert_array_equal(x["ok"], np.arange(7) % 2)
+        assert float(x["t_max"]) == 1.0 and float(x["it_sum"]) == 7
+
+
+def test_shard_tiles_batch():
+    from irm_motion_planning_amd.distributed import shard
+    for B in (1, 7, 8, 1024, 8193):
+        for world in (1, 2, 3, 8):
+            rs = [shard(B, world, r) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == B
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+            assert max(h - l for l, h in rs) - min(h - l for l, h in rs) <= 1

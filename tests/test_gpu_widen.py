@@ -240,3 +240,31 @@ def test_whole_robot_bls_end_to_end():
     c_ee = Context(params())
     a_ee, _, _ = c_ee.optimize(START, GOAL, obs)
     assert avg < c.eval_cost(a_ee, obs, START, GOAL, 0, 0, 0)
+
+
+def test_main_cli_two_ranks_sharded(tmp_path):
+    """torchrun, 2 ranks (sharing the box's one GPU, host-side gloo collectives): the sharded
+    batch run writes the same batch files as the single-process run (per-problem results are
+    independent of batch neighbours up to summation-tile differences, 1e-4)."""
+    import subprocess
+    import sys
+    from irm_motion_planning_amd import batch_io
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    argv = list(GD20) + ["--batch-size", "9", "--seed", "5"]
+    d1, d2 = tmp_path / "one", tmp_path / "two"
+    d1.mkdir()
+    d2.mkdir()
+    env = dict(os.environ, PYTHONPATH=repo, IRM_DIST_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    subprocess.run([sys.executable, "-m", "irm_motion_planning_amd.main"] + argv, cwd=d1, env=env, check=True,
+                   timeout=300)
+    port = 29500 + os.getpid() % 1000
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                    "--master-addr", "127.0.0.1", "--master-port", str(port), "-m",
+                    "irm_motion_planning_amd.main"] + argv, cwd=d2, env=env, check=True, timeout=300)
+    a = batch_io.read_result_batch(d1 / batch_io.RESULT_BATCH, 50, 3)
+    b = batch_io.read_result_batch(d2 / batch_io.RESULT_BATCH, 50, 3)
+    assert a.shape == b.shape == (9, 50, 3)
+    np.testing.assert_allclose(b, a, rtol=0, atol=1e-4)
+    sa, sb = np.loadtxt(d1 / batch_io.SUMMARY_BATCH), np.loadtxt(d2 / batch_io.SUMMARY_BATCH)
+    np.testing.assert_array_equal(sa[:, 2:], sb[:, 2:])  # flags and iteration counts
