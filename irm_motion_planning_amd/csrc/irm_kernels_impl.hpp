@@ -116,6 +116,9 @@ struct Prof {
         acc[ph] += now - last;
         last = now;
     }
+    __device__ __forceinline__ void count(int ph, bool c) {
+        if (c) acc[ph] += 1;
+    }
     __device__ __forceinline__ void flush(unsigned long long* out) {
         if (out)
             for (int i = 0; i < kProfPhases; ++i) out[(size_t)blockIdx.x * kProfPhases + i] = acc[i];
@@ -123,15 +126,21 @@ struct Prof {
 #else
     __device__ __forceinline__ void init() {}
     __device__ __forceinline__ void stamp(int) {}
+    __device__ __forceinline__ void count(int, bool) {}
     __device__ __forceinline__ void flush(unsigned long long*) {}
 #endif
 };
 #ifdef IRM_ISA_MARKS  // analysis builds: phase markers in the emitted assembly
 #define IRM_STAMP(ph) asm volatile("; IRM_PHASE " #ph)
+#define IRM_COUNT(ph, c)
 #else
 #define IRM_STAMP(ph)                         \
     do {                                      \
         if (threadIdx.x == 0) prof.stamp(ph); \
+    } while (0)
+#define IRM_COUNT(ph, c)                          \
+    do {                                          \
+        if (threadIdx.x == 0) prof.count(ph, c);  \
     } while (0)
 #endif
 
@@ -580,12 +589,15 @@ struct FixShape {
     static constexpr int D = D_, N = N_, NK = (N_ + 15) / 16 * 16, MP = 2 * NK, RP = RP_;
     static constexpr int NW = (N_ + 63) / 64 * 64, WPT = NW / 64, NSPLIT = stage1_splits(NK);
     static constexpr bool kVariants = false;  // end-effector cost only (the reference's)
+    // stage-1 k-quads per split-K unit when the split is even (else 0: checked per quad)
+    static constexpr int KQU = (NK / 16) % NSPLIT == 0 ? (NK / 16) / NSPLIT : 0;
     __device__ explicit FixShape(const KParams&) {}
 };
 template <int D_>
 struct DynShape {
     static constexpr int D = D_;
     static constexpr bool kVariants = true;  // cost variants chosen at run time (whole_robot)
+    static constexpr int KQU = 0;
     int N, NK, MP, RP, NW, WPT, NSPLIT;
     __device__ explicit DynShape(const KParams& P)
         : N(P.N), NK(P.NK), MP(P.MP), RP(P.RP), NW(P.NW), WPT(P.NW >> 6), NSPLIT(P.nsplit) {}
@@ -671,7 +683,10 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_optimize(KParams 
         F1 = smem + L.f1;
         F2 = smem + L.f2;
     }
-    f32x4 a1[REGOPS ? S1Q : 1], a2[REGOPS ? S2T * 2 : 1];
+    // RV: the velocity half of stage 1's fragments is register-resident too (dense rounds, where
+    // b' is non-zero away from the endpoints, then read no operator from memory)
+    constexpr bool RV = REGOPS && MAXT > 256;
+    f32x4 a1[REGOPS ? S1Q : 1], a2[REGOPS ? S2T * 2 : 1], a1v[RV ? S1Q : 1];
     if (REGOPS) {  // operator A-fragments resident in VGPRs for the whole launch
         const f32x4* g1 = reinterpret_cast<const f32x4*>(P.F1frag);
         const f32x4* g2 = reinterpret_cast<const f32x4*>(P.F2frag);
@@ -679,6 +694,10 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_optimize(KParams 
         for (int i = 0; i < S1Q; ++i) {
             a1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
             if (has1 && kq0 + i < kq1) a1[i] = g1[((size_t)tile1 * KQ1 + kq0 + i) * 64 + lane];
+            if constexpr (RV) {
+                a1v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (has1 && kq0 + i < kq1) a1v[i] = g1[((size_t)tile1 * KQ1 + KQa + kq0 + i) * 64 + lane];
+            }
         }
 #pragma unroll
         for (int j = 0; j < S2T; ++j)
@@ -773,29 +792,57 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_optimize(KParams 
         };
         if (REGOPS) {  // one unit per wave (regops_fit), position-half fragments in VGPRs
             if (has1) {
-                float bv[S1Q][4];
+                // k-quads of this unit: compile-time count for the shape-specialised kernels
+                constexpr bool kFix = S::KQU > 0 && S::KQU <= S1Q;
+                constexpr int KQU = kFix ? S::KQU : S1Q;
+                auto in = [&](int i) { return kFix ? i < KQU : kq0 + i < kq1; };
+                float bv[KQU][4], bw[RV ? KQU : 1][4];
 #pragma unroll
-                for (int i = 0; i < S1Q; ++i) {
+                for (int i = 0; i < KQU; ++i) {
                     const float* xb = xl + (kq0 + i) * 16 * kLd;
-                    const bool in = kq0 + i < kq1;
-                    bv[i][0] = in ? xb[0] : 0.f;
-                    bv[i][1] = in ? xb[4 * kLd] : 0.f;
-                    bv[i][2] = in ? xb[8 * kLd] : 0.f;
-                    bv[i][3] = in ? xb[12 * kLd] : 0.f;
+                    bv[i][0] = in(i) ? xb[0] : 0.f;
+                    bv[i][1] = in(i) ? xb[4 * kLd] : 0.f;
+                    bv[i][2] = in(i) ? xb[8 * kLd] : 0.f;
+                    bv[i][3] = in(i) ? xb[12 * kLd] : 0.f;
+                }
+                if constexpr (RV) {
+                    if (full) {
+#pragma unroll
+                        for (int i = 0; i < KQU; ++i) {
+                            const float* xb = xl + (KQa + kq0 + i) * 16 * kLd;
+                            bw[i][0] = in(i) ? xb[0] : 0.f;
+                            bw[i][1] = in(i) ? xb[4 * kLd] : 0.f;
+                            bw[i][2] = in(i) ? xb[8 * kLd] : 0.f;
+                            bw[i][3] = in(i) ? xb[12 * kLd] : 0.f;
+                        }
+                    }
                 }
                 f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int i = 0; i < S1Q; ++i) {
-                    if (kq0 + i < kq1) {
+                for (int i = 0; i < KQU; ++i) {
+                    if (in(i)) {
                         acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][0], bv[i][0], acc0, 0, 0, 0);
                         acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][1], bv[i][1], acc1, 0, 0, 0);
                         acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][2], bv[i][2], acc0, 0, 0, 0);
                         acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][3], bv[i][3], acc1, 0, 0, 0);
                     }
                 }
-                if (full)
+                if constexpr (RV) {
+                    if (full) {
+#pragma unroll
+                        for (int i = 0; i < KQU; ++i) {
+                            if (in(i)) {
+                                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1v[i][0], bw[i][0], acc0, 0, 0, 0);
+                                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1v[i][1], bw[i][1], acc1, 0, 0, 0);
+                                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1v[i][2], bw[i][2], acc0, 0, 0, 0);
+                                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1v[i][3], bw[i][3], acc1, 0, 0, 0);
+                            }
+                        }
+                    }
+                } else if (full) {
                     quads(reinterpret_cast<const f32x4*>(F1) + ((size_t)tile1 * KQ1 + KQa) * 64 + lane, KQa, kq0,
                           kq1, acc0, acc1);
+                }
                 store_tile(Ypart + sp1 * RP * kLd, tile1, acc0 + acc1, 0xFFFFu);
             }
         } else {
@@ -848,6 +895,8 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_optimize(KParams 
                     e1[k] = X[(NK + N - 1) * kLd + t * D + k];
                 }
             }
+            IRM_STAMP(1);
+            IRM_COUNT(13, dense);
             stage1(dense);
             IRM_STAMP(5);
             __syncthreads();
@@ -1245,7 +1294,6 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_optimize(KParams 
         }
     }
     if (P.stats && tvalid && n == 0) P.stats[b] = st;
-    IRM_STAMP(13);
     if (tid == 0) prof.flush(P.prof);
 }
 

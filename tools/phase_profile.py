@@ -16,9 +16,9 @@ import bench  # noqa: E402
 from irm_motion_planning_amd.context import Context  # noqa: E402
 from irm_motion_planning_amd.params import params_from_args  # noqa: E402
 
-PHASES = ["dir:stage1 barrier-wait", "(unused)", "dir:y rows + BLS norms", "dir:stage2 + barrier", "round-top (flags)",
+PHASES = ["dir:stage1 barrier-wait", "dir: latch + endpoint reads", "dir:y rows + BLS norms", "dir:stage2 + barrier", "round-top (flags)",
           "dir:endpoint + stage1 mfma", "post-dir + resync + update", "E1 barrier-wait", "eval_waypoint",
-          "eval reductions", "finalize+decide", "end barrier-wait", "grad inputs (mixed) + b flag", "epilogue",
+          "eval reductions", "finalize+decide", "end barrier-wait", "grad inputs (mixed) + b flag", "#rounds with dense stage 1 (count)",
           "prologue", "accept+yacc+flags"]
 
 
@@ -36,12 +36,14 @@ def run(cfg, tb=0, rank=0, faithful=False):
     n = ctx.lib.irm_debug_phase_profile(ctx.handle, buf, nb)
     prof = np.frombuffer(buf, dtype=np.uint64, count=n * 16).reshape(n, 16).astype(np.float64)
     rounds = float(np.max(st["grad_evals"]) + np.max(st["outer_iterations"]))
-    tot = prof.sum(1)
+    tot = prof.sum(1) - prof[:, 13]
     print(f"== {cfg} tb={info['traj_per_block']} R={info['operator_rank']} blocks={n} host {1000*dt:.2f} ms "
           f"rounds~{rounds:.0f} total cycles/block mean {tot.mean():.0f} -> {tot.mean()/rounds:.0f} per round")
     for i, name in enumerate(PHASES):
         c = prof[:, i].mean()
-        if c > 0:
+        if i == 13:
+            print(f"   {name:22s} {c:9.1f} of {rounds:.0f} rounds")
+        elif c > 0:
             print(f"   {name:22s} {c/rounds:9.0f} cyc/round  ({100*c/tot.mean():5.1f} %)")
 
 
