@@ -223,7 +223,7 @@ int irm_optimize_batch_dev(irm_ctx* ctx, const irm_batch_dev* args, void* stream
 int32_t irm_series_capacity(const irm_ctx* ctx);
 
 /* Diagnostics: per-workgroup phase cycle counters of the last optimize
- * launch (16 uint64 per workgroup).  Only a library built with
+ * launch (24 uint64 per workgroup).  Only a library built with
  * -DIRM_PHASE_PROFILE records them; otherwise returns IRM_EINVAL.  Returns
  * the number of workgroups written. */
 int irm_debug_phase_profile(irm_ctx* ctx, uint64_t* out, int32_t max_blocks);

@@ -84,7 +84,7 @@ struct KParams {
     unsigned long long* prof;  // IRM_PHASE_PROFILE builds: per-block phase cycle counters
 };
 
-constexpr int kProfPhases = 16;
+constexpr int kProfPhases = 24;
 
 // Operator fragment sizes (floats) for the layout of mfma_frag_index.
 __host__ __device__ inline int64_t frag_floats(int M, int K) {

@@ -622,7 +622,9 @@ constexpr int kS2T(int maxt) { return maxt <= 256 ? 8 : 2; }   // stage-2 tiles 
 // steps (acc = c·acc + s·[a'; b']), and α = cprod·α_base − V_R·Fᵀ·acc·J⁻¹ is
 // formed only when an inner loop ends (PH_RESYNC).
 template <class S, int MAXT, bool OPS_LDS, bool REGOPS, bool BLS>
-__global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_optimize(KParams P) {
+// 256-thread workgroups without register-resident operators fit two per CU (≤ 256 VGPRs); the
+// REGOPS variants need more and keep one (they are launched one per CU anyway).
+__global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_optimize(KParams P) {
     constexpr int D = S::D;
     constexpr int S1Q = kS1Q(MAXT), S2T = kS2T(MAXT);
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -685,7 +687,7 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_optimize(KParams 
     }
     // RV: the velocity half of stage 1's fragments is register-resident too (dense rounds, where
     // b' is non-zero away from the endpoints, then read no operator from memory)
-    constexpr bool RV = REGOPS && MAXT > 256;
+    constexpr bool RV = REGOPS && MAXT > 256 && !BLS;  // (the BLS state leaves no room: spills)
     f32x4 a1[REGOPS ? S1Q : 1], a2[REGOPS ? S2T * 2 : 1], a1v[RV ? S1Q : 1];
     if (REGOPS) {  // operator A-fragments resident in VGPRs for the whole launch
         const f32x4* g1 = reinterpret_cast<const f32x4*>(P.F1frag);
@@ -885,12 +887,15 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_optimize(KParams 
         if (dirmask) {
             // the direction's gradient inputs: this lane's rows (α recovery) and the two
             // endpoint velocity rows of its trajectory (sparse stage 1)
-            float e0[D], e1[D];
-            if (needs_dir) {
+            // issued unconditionally (no branch, so the waits move to the first use after the
+            // stage-1 barrier); rows of invalid lanes are clamped and their values discarded
+            float e0[D], e1[D], xa[D], xb[D];
+            {
+                const int nr = valid ? n : 0;
 #pragma unroll
                 for (int k = 0; k < D; ++k) {
-                    dra[k] = valid ? X[n * kLd + t * D + k] : 0.f;
-                    drb[k] = valid ? X[(NK + n) * kLd + t * D + k] : 0.f;
+                    xa[k] = X[nr * kLd + t * D + k];
+                    xb[k] = X[(NK + nr) * kLd + t * D + k];
                     e0[k] = X[NK * kLd + t * D + k];
                     e1[k] = X[(NK + N - 1) * kLd + t * D + k];
                 }
@@ -993,6 +998,8 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_optimize(KParams 
                 // latch this lane's direction rows (+ the endpoint-velocity columns)
 #pragma unroll
                 for (int k = 0; k < D; ++k) {
+                    dra[k] = valid ? xa[k] : 0.f;
+                    drb[k] = valid ? xb[k] : 0.f;
                     float ut = dP[n * kLd + t * D + k], uv = dP[(NK + n) * kLd + t * D + k];
                     if (!dense) {
                         ut = fmaf(h0T, e0[k], fmaf(h1T, e1[k], ut));
@@ -1001,6 +1008,7 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_optimize(KParams 
                     dT[k] = ut;
                     dV[k] = uv;
                 }
+                IRM_STAMP(16);
                 if (bls) {
                     float tg = 0.f, ta = 0.f;
                     for (int ww = 0; ww < WPT; ++ww) {
@@ -1086,6 +1094,7 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_optimize(KParams 
                 for (int k = 0; k < D; ++k) aca[k] = acb[k] = 0.f;
             }
         }
+        IRM_STAMP(17);
         // ------------------------------------------------------- update
         float q2[D], v2[D];
         if (phase == PH_GD_INNER || phase == PH_BLS_TRIAL) {
@@ -1143,6 +1152,7 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_optimize(KParams 
                 va = fmaxf(va, rw[5]);
             }
             const float e_a0 = sg[t * 4 + 0], e_b0 = sg[t * 4 + 1], e_a1 = sg[t * 4 + 2], e_b1 = sg[t * 4 + 3];
+            IRM_STAMP(18);
             const float sgpc = 0.5f * e_a0 + 0.5f * e_a1;                       // trajectory.py:187
             const float sgvc = 0.5f * e_b0 + 0.5f * e_b1;                       // trajectory.py:203
             // trajectory.py:85-87 + 281 (mean and joint-limit terms pre-summed in usum)

@@ -19,7 +19,8 @@ from irm_motion_planning_amd.params import params_from_args  # noqa: E402
 PHASES = ["dir:stage1 barrier-wait", "dir: latch + endpoint reads", "dir:y rows + BLS norms", "dir:stage2 + barrier", "round-top (flags)",
           "dir:endpoint + stage1 mfma", "post-dir + resync + update", "E1 barrier-wait", "eval_waypoint",
           "eval reductions", "finalize+decide", "end barrier-wait", "grad inputs (mixed) + b flag", "#rounds with dense stage 1 (count)",
-          "prologue", "accept+yacc+flags"]
+          "prologue", "accept+yacc+flags", "dP latch (after stage-2 barrier)", "resync check",
+          "finalize: partial reads"]
 
 
 def run(cfg, tb=0, rank=0, faithful=False):
@@ -32,9 +33,10 @@ def run(cfg, tb=0, rank=0, faithful=False):
     alpha, traj, st = ctx.optimize(start, goal, obstacles)
     dt = time.perf_counter() - t0
     nb = 4096
-    buf = (ctypes.c_uint64 * (nb * 16))()
+    K = 24
+    buf = (ctypes.c_uint64 * (nb * K))()
     n = ctx.lib.irm_debug_phase_profile(ctx.handle, buf, nb)
-    prof = np.frombuffer(buf, dtype=np.uint64, count=n * 16).reshape(n, 16).astype(np.float64)
+    prof = np.frombuffer(buf, dtype=np.uint64, count=n * K).reshape(n, K).astype(np.float64)
     rounds = float(np.max(st["grad_evals"]) + np.max(st["outer_iterations"]))
     tot = prof.sum(1) - prof[:, 13]
     print(f"== {cfg} tb={info['traj_per_block']} R={info['operator_rank']} blocks={n} host {1000*dt:.2f} ms "
