@@ -35,6 +35,9 @@ CONFIGS = {
     "c5": ("7-DoF arm, batch of 512 per GPU (4096 on 8), N=256, 11 obstacles, GD (BASELINE configs[4])",
            512, 256, 7, 11, "gd"),
     "c2": ("single trajectory, N=128, 10 obstacles, BLS (BASELINE configs[1])", 1, 128, 3, 10, "bls"),
+    # diagnostic shapes (not BASELINE configurations): C3's batch at other trajectory lengths
+    "c3n64": ("diagnostic: C3 batch at N=64", 1024, 64, 3, 11, "gd"),
+    "c3n256": ("diagnostic: C3 batch at N=256", 1024, 256, 3, 11, "gd"),
 }
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X fp32 (vector = matrix), MI355X_MICROARCH.md
@@ -54,7 +57,7 @@ def make_problem(cfg, world, rank):
                 obs.append(o)
         obstacles = np.array(obs, np.float32)
         rs = np.random.default_rng(3)
-    else:
+    else:  # c3, c5, c2 and the diagnostic c3n* shapes
         from irm_motion_planning_amd.environment import OBSTACLES
         obstacles = OBSTACLES[:O].astype(np.float32)
         rs = np.random.default_rng(4 if cfg == "c5" else 1)

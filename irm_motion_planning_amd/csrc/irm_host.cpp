@@ -11,6 +11,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -632,6 +633,10 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
     kp.one_m_lmax = (float)(1.0 - (double)p->lambda_max_cost);
     kp.record_series = p->record_series ? 1 : 0;
     kp.whole_robot = p->whole_robot_cost ? 1 : 0;
+    {
+        const char* g = getenv("IRM_GENERAL_KERNEL");  // diagnostics: force the general optimiser
+        kp.lean_ok = (g && g[0] == '1') ? 0 : 1;
+    }
     c->max_series = p->max_series > 0 ? p->max_series : 1 + p->max_outer_iteration * p->max_inner_iteration;
     kp.max_series = c->max_series;
 

@@ -39,7 +39,8 @@ struct KParams {
     int32_t nsplit;      // stage-1 split-K factor
     int32_t regops;      // operator A-fragments held in VGPRs (k_optimize<…, REGOPS>)
     // optimiser
-    int32_t optimizer, max_inner, max_outer, max_bls, cvdl, record_series, max_series, pad0;
+    int32_t optimizer, max_inner, max_outer, max_bls, cvdl, record_series, max_series;
+    int32_t lean_ok;  // k_gd_single may serve GD single-loop launches (IRM_GENERAL_KERNEL=1 clears it)
     float llr, lci, lsg0, ljl0, eps_p, eps_v, lmax, lreg;
     float bls_lr0, bls_a, bls_bp, bls_bm, vmax, pmax, pmin, pad1;
     // derived fp32 constants (reference casts its Python doubles to fp32)

@@ -1307,6 +1307,426 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
     if (tid == 0) prof.flush(P.prof);
 }
 
+// ------------------------------------------- GD single loop, lean optimiser
+// optimizer_GD.py jit_optimize (max_outer_iteration == 1, dualOptimization false;
+// optimizer_GD.py:281-310): g = ∇L(α); α' = (1 − λ_reg·lr)·α − lr·g; accept iff
+// L − L(α') ≥ loop_loss_reduction, else stop keeping α; at most max_inner steps; then
+// α is materialised and constraintsFulfilled decides constraints_ok (k_optimize's
+// PH_RESYNC).  The same arithmetic as k_optimize's GD rounds (bit-identical results,
+// tests/test_gpu_parity.py::test_lean_gd_kernel_equals_general) without the general
+// state machine: every trajectory is either stepping or done, so a round needs no
+// phase logic, no direction / resync masks and no LDS atomics — per-wave flag words
+// (done, b' non-zero away from the endpoints) are read by every wave after the end
+// barrier.  Shape-specialised, operators register-resident (REGOPS) only.
+template <class S, int MAXT>
+__global__ __launch_bounds__(MAXT) void k_gd_single(KParams P) {
+    constexpr int D = S::D;
+    constexpr int S1Q = kS1Q(MAXT), S2T = kS2T(MAXT);
+    constexpr bool RV = MAXT > 256;  // velocity half of stage 1 register-resident too
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const S sh(P);
+    const Head H = plan_head(sh.MP, sh.RP, sh.NSPLIT, true);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nwaves = P.BT >> 6;
+    const int N = sh.N, NW = sh.NW, TB = P.TB, RP = sh.RP, MP = sh.MP, NK = sh.NK;
+    const int WPT = sh.WPT;
+    const int t = wave / WPT;
+    const int n = tid - t * NW;
+    const int n0 = (wave - t * WPT) * 64;
+    const int tb0 = blockIdx.x * TB;
+    const int ntb = min(TB, P.B - tb0);
+    if (ntb <= 0) return;
+    const bool tvalid = t < ntb;
+    const bool valid = tvalid && n < N;
+    const bool yrow = tvalid && n < RP;
+    const size_t b = (size_t)(tb0 + (tvalid ? t : 0));
+
+    float* X = smem + H.X;
+    float* dP = smem + H.dP;
+    float* Ypart = smem + H.Ypart;
+    float* Ymix = smem + H.Ymix;
+    float* red = smem + H.red;
+    float* sg = smem + H.sg;
+    unsigned* wflag = reinterpret_cast<unsigned*>(smem + H.wp);  // per wave: bit 0 done, bit 1 b' far
+    float* obsL = smem + H.obs;
+
+    const int KQ1 = MP / 16, KQa = NK / 16, MT1 = RP / 16, KQ2 = RP / 16, MT2 = MP / 16;
+    const int nsplit = sh.NSPLIT;
+    const bool has1 = wave < MT1 * nsplit;
+    const int tile1 = wave % MT1, sp1 = wave / MT1;
+    const int kq0 = (KQa * sp1) / nsplit, kq1 = (KQa * (sp1 + 1)) / nsplit;
+
+    // ----------------------------------------------------------- prologue
+    f32x4 a1[S1Q], a1v[RV ? S1Q : 1], a2[S2T * 2];
+    {
+        const f32x4* g1 = reinterpret_cast<const f32x4*>(P.F1frag);
+        const f32x4* g2 = reinterpret_cast<const f32x4*>(P.F2frag);
+#pragma unroll
+        for (int i = 0; i < S1Q; ++i) {
+            a1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (has1 && kq0 + i < kq1) a1[i] = g1[((size_t)tile1 * KQ1 + kq0 + i) * 64 + lane];
+            if constexpr (RV) {
+                a1v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (has1 && kq0 + i < kq1) a1v[i] = g1[((size_t)tile1 * KQ1 + KQa + kq0 + i) * 64 + lane];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < S2T; ++j)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                a2[j * 2 + i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                const int tile = wave + j * nwaves;
+                if (tile < MT2 && i < KQ2) a2[j * 2 + i] = g2[((size_t)tile * KQ2 + i) * 64 + lane];
+            }
+    }
+    const float h0T = valid ? P.Hend[n] : 0.f, h1T = valid ? P.Hend[MP + n] : 0.f;
+    const float h0V = valid ? P.Hend[NK + n] : 0.f, h1V = valid ? P.Hend[MP + NK + n] : 0.f;
+    stage_obstacles(P, tb0, ntb, obsL);
+    stage_alpha<D>(P, tb0, ntb, X, NK);
+    __syncthreads();
+    float q[D], v[D], s[D], g[D], ab[D], dra[D], drb[D], aca[D], acb[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        q[k] = v[k] = 0.f;
+        dra[k] = drb[k] = aca[k] = acb[k] = 0.f;
+        ab[k] = valid ? X[n * kLd + t * D + k] : 0.f;
+        s[k] = tvalid ? P.start[b * D + k] : 0.f;
+        g[k] = tvalid ? P.goal[b * D + k] : 0.f;
+    }
+    if (valid) eval_exact<D>(P, X + t * D, n, q, v);  // T0 = (K·α0)·J, V0 = (dK·α0)·J
+    __syncthreads();
+    for (int e = tid; e < MP * kLd; e += P.BT) X[e] = 0.f;
+    const float* obs = obsL + (P.obs_stride ? t * obs_pitch(P.O) : 0);
+    const float lsg = P.lsg0, ljl = P.ljl0, lr = P.gd_lr[0];
+    const float cfac = 1.f - P.lreg * lr, step = lr;
+
+    // evaluation of (q2, v2) with this trajectory's waves: wave partials + endpoint rows
+    auto evaluate = [&](const float (&q2)[D], const float (&v2)[D], bool ext, WP<D>& w) {
+        if (valid) eval_waypoint<D>(P, q2, v2, obs, w);
+        const float us = P.one_m_lmax * (w.cv * P.invN) + ljl * ((w.jp + w.jv) * P.invN);
+        ered_store(valid, w.cv, us, w.tx, w.tn, w.va, ext, n0, red, wave);
+        if (valid && (n == 0 || n == N - 1)) {  // trajectory.py:183-204 rows 0 and N−1
+            float a = 0.f, bb = 0.f;
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const float e = q2[d] - (n == 0 ? s[d] : g[d]);
+                a += e * e;
+                bb += v2[d] * v2[d];
+            }
+            sg[t * 4 + (n == 0 ? 0 : 2)] = a;
+            sg[t * 4 + (n == 0 ? 1 : 3)] = bb;
+        }
+    };
+    struct Fin {
+        float nl, tx, tn, va, a0, b0, a1, b1;
+        int idx;
+    };
+    auto finalize = [&]() {
+        const float* r0 = red + (t * WPT) * 8;
+        float cmax = r0[0];
+        int cidx = __float_as_int(r0[1]);
+        float usum = r0[2], tx = r0[3], tn = r0[4], va = r0[5];
+        for (int ww = 1; ww < WPT; ++ww) {
+            const float* rw = red + (t * WPT + ww) * 8;
+            amax_step(cmax, cidx, rw[0], __float_as_int(rw[1]));
+            usum += rw[2];
+            tx = fmaxf(tx, rw[3]);
+            tn = fminf(tn, rw[4]);
+            va = fmaxf(va, rw[5]);
+        }
+        Fin f;
+        f.a0 = sg[t * 4 + 0];
+        f.b0 = sg[t * 4 + 1];
+        f.a1 = sg[t * 4 + 2];
+        f.b1 = sg[t * 4 + 3];
+        const float sgpc = 0.5f * f.a0 + 0.5f * f.a1;  // trajectory.py:187
+        const float sgvc = 0.5f * f.b0 + 0.5f * f.b1;  // trajectory.py:203
+        f.nl = (P.lam_max * cmax + usum) + lsg * (sgpc + sgvc);
+        f.idx = cidx;
+        f.tx = tx;
+        f.tn = tn;
+        f.va = va;
+        return f;
+    };
+    // gradient inputs at (q2, v2), mixed by JᵀJ, into X; returns "b' non-zero away from the endpoints"
+    auto grad_inputs = [&](const WP<D>& w, const float (&q2)[D], const float (&v2)[D], int cidx) {
+        bool bfar = false;
+        if (valid) {
+            float a[D], bb[D];
+            grad_waypoint<D>(P, w, q2, v2, n, cidx, lsg, ljl, s, g, a, bb);
+            const bool endrow = (n == 0 || n == N - 1);
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                float ma = 0.f, mb = 0.f;
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    ma += a[d] * P.JtJ[d * D + k];
+                    mb += bb[d] * P.JtJ[d * D + k];
+                }
+                X[n * kLd + t * D + k] = ma;
+                X[(NK + n) * kLd + t * D + k] = mb;
+                bfar |= (!endrow && bb[k] != 0.f);
+            }
+        }
+        return __ballot(bfar) != 0ull;
+    };
+    auto stage1 = [&](bool full) {  // Ypart[sp] = Fᵀ·[a'; b'] over this wave's unit
+        if (!has1) return;
+        const float* xl = X + (lane >> 4) * kLd + (lane & 15);
+        constexpr bool kFix = S::KQU > 0 && S::KQU <= S1Q;
+        constexpr int KQU = kFix ? S::KQU : S1Q;
+        auto in = [&](int i) { return kFix ? i < KQU : kq0 + i < kq1; };
+        float bv[KQU][4], bw[RV ? KQU : 1][4];
+#pragma unroll
+        for (int i = 0; i < KQU; ++i) {
+            const float* xb = xl + (kq0 + i) * 16 * kLd;
+            bv[i][0] = in(i) ? xb[0] : 0.f;
+            bv[i][1] = in(i) ? xb[4 * kLd] : 0.f;
+            bv[i][2] = in(i) ? xb[8 * kLd] : 0.f;
+            bv[i][3] = in(i) ? xb[12 * kLd] : 0.f;
+        }
+        if constexpr (RV) {
+            if (full) {
+#pragma unroll
+                for (int i = 0; i < KQU; ++i) {
+                    const float* xb = xl + (KQa + kq0 + i) * 16 * kLd;
+                    bw[i][0] = in(i) ? xb[0] : 0.f;
+                    bw[i][1] = in(i) ? xb[4 * kLd] : 0.f;
+                    bw[i][2] = in(i) ? xb[8 * kLd] : 0.f;
+                    bw[i][3] = in(i) ? xb[12 * kLd] : 0.f;
+                }
+            }
+        }
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < KQU; ++i) {
+            if (in(i)) {
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][0], bv[i][0], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][1], bv[i][1], acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][2], bv[i][2], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][3], bv[i][3], acc1, 0, 0, 0);
+            }
+        }
+        if (full) {
+            if constexpr (RV) {
+#pragma unroll
+                for (int i = 0; i < KQU; ++i) {
+                    if (in(i)) {
+                        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1v[i][0], bw[i][0], acc0, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1v[i][1], bw[i][1], acc1, 0, 0, 0);
+                        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1v[i][2], bw[i][2], acc0, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1v[i][3], bw[i][3], acc1, 0, 0, 0);
+                    }
+                }
+            } else {
+                const f32x4* ap = reinterpret_cast<const f32x4*>(P.F1frag) + ((size_t)tile1 * KQ1 + KQa) * 64 + lane;
+                for (int kq = kq0; kq < kq1; ++kq) {
+                    const f32x4 a = ap[(size_t)kq * 64];
+                    const float* xb = xl + (KQa + kq) * 16 * kLd;
+                    const float b0 = xb[0], b1 = xb[4 * kLd], b2 = xb[8 * kLd], b3 = xb[12 * kLd];
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b0, acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b1, acc1, 0, 0, 0);
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b2, acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b3, acc1, 0, 0, 0);
+                }
+            }
+        }
+        store_tile(Ypart + sp1 * RP * kLd, tile1, acc0 + acc1, 0xFFFFu);
+    };
+
+    // round 0 (optimizer_GD.py:295: the loss at α0) and the first gradient inputs
+    irm_stats st{};
+    float loss;
+    bool done = !tvalid;
+    {
+        WP<D> w;
+        evaluate(q, v, false, w);
+        __syncthreads();
+        const Fin f = finalize();
+        loss = f.nl;
+        st.cost_evals = 1;
+        if (P.max_inner <= 0) done = true;
+        const bool bfar = grad_inputs(w, q, v, f.idx);
+        if (lane == 0) wflag[wave] = (done ? 1u : 0u) | (bfar ? 2u : 0u);
+    }
+    __syncthreads();
+
+    // ---------------------------------------------------------- GD rounds
+    int inner = 0;
+    float cprod = 1.f;
+    for (;;) {
+        unsigned fl = 0xFFFFFFFFu, any = 0u;
+        for (int w2 = 0; w2 < nwaves; ++w2) {
+            const unsigned x = wflag[w2];
+            fl &= x;
+            any |= x;
+        }
+        if (fl & 1u) break;  // every trajectory of the block is done
+        const bool dense = (any & 2u) != 0u;
+        // this lane's gradient-input rows (α recovery) and the endpoint velocity rows
+        float e0[D], e1[D], xa[D], xb[D];
+        {
+            const int nr = valid ? n : 0;
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                xa[k] = X[nr * kLd + t * D + k];
+                xb[k] = X[(NK + nr) * kLd + t * D + k];
+                e0[k] = X[NK * kLd + t * D + k];
+                e1[k] = X[(NK + N - 1) * kLd + t * D + k];
+            }
+        }
+        stage1(dense);
+        __syncthreads();
+        {  // stage 2: dP = F·Σ_s Ypart[s]
+            const float* xl = Ypart + (lane >> 4) * kLd + (lane & 15);
+            f32x4 acc[S2T];
+#pragma unroll
+            for (int j = 0; j < S2T; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            float bv[2][4];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                bv[i][0] = bv[i][1] = bv[i][2] = bv[i][3] = 0.f;
+                if (i < KQ2) {
+                    for (int sp = 0; sp < nsplit; ++sp) {
+                        const float* x = xl + (sp * RP + i * 16) * kLd;
+                        bv[i][0] += x[0];
+                        bv[i][1] += x[4 * kLd];
+                        bv[i][2] += x[8 * kLd];
+                        bv[i][3] += x[12 * kLd];
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                if (i < KQ2) {
+#pragma unroll
+                    for (int j = 0; j < S2T; ++j) {
+                        if (wave + j * nwaves < MT2) {
+                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][0], bv[i][0], acc[j], 0, 0, 0);
+                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][1], bv[i][1], acc[j], 0, 0, 0);
+                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][2], bv[i][2], acc[j], 0, 0, 0);
+                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][3], bv[i][3], acc[j], 0, 0, 0);
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < S2T; ++j)
+                if (wave + j * nwaves < MT2) store_tile(dP, wave + j * nwaves, acc[j], 0xFFFFu);
+        }
+        __syncthreads();
+        float q2[D], v2[D];
+        WP<D> w;
+        if (!done) {  // wave-uniform
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                float ut = dP[n * kLd + t * D + k], uv = dP[(NK + n) * kLd + t * D + k];
+                if (!dense) {
+                    ut = fmaf(h0T, e0[k], fmaf(h1T, e1[k], ut));
+                    uv = fmaf(h0V, e0[k], fmaf(h1V, e1[k], uv));
+                }
+                dra[k] = valid ? xa[k] : 0.f;
+                drb[k] = valid ? xb[k] : 0.f;
+                q2[k] = cfac * q[k] - step * ut;
+                v2[k] = cfac * v[k] - step * uv;
+            }
+            evaluate(q2, v2, false, w);
+        }
+        __syncthreads();
+        if (!done) {
+            const Fin f = finalize();
+            st.grad_evals++;
+            st.cost_evals++;
+            bool bfar = false;
+            if (loss - f.nl < P.llr) {
+                done = true;  // minimized: the step is discarded (optimizer_GD.py:304-306)
+            } else {
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    q[k] = q2[k];
+                    v[k] = v2[k];
+                    aca[k] = cfac * aca[k] + step * dra[k];  // α recovery: Σ steps·[a'; b']
+                    acb[k] = cfac * acb[k] + step * drb[k];
+                }
+                cprod *= cfac;
+                loss = f.nl;
+                inner++;
+                st.inner_iterations++;
+                if (inner >= P.max_inner) done = true;
+                else bfar = grad_inputs(w, q2, v2, f.idx);
+            }
+            if (lane == 0) wflag[wave] = (done ? 1u : 0u) | (bfar ? 2u : 0u);
+        }
+        __syncthreads();
+    }
+
+    // ---------------------------------------------------------- epilogue
+    // α = cprod·α0 − V_R·(Fᵀ·acc)·J⁻¹ in fp32 (k_optimize's PH_RESYNC), T = eval_exact(α),
+    // constraintsFulfilled(α) (trajectory.py:129-137, robot.py:90-113).
+    st.final_loss = loss;
+    if (valid) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            X[n * kLd + t * D + k] = aca[k];
+            X[(NK + n) * kLd + t * D + k] = acb[k];
+        }
+    }
+    __syncthreads();
+    stage1(true);
+    __syncthreads();
+    if (yrow) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            float y = 0.f;
+            for (int sp = 0; sp < nsplit; ++sp) y += Ypart[(sp * RP + n) * kLd + t * D + d];
+            Ymix[n * kLd + t * D + d] = y;
+        }
+    }
+    __syncthreads();
+    if (valid) {
+        float z[D];
+#pragma unroll
+        for (int l = 0; l < D; ++l) z[l] = 0.f;
+        const float* vr = P.Vr + (size_t)n * RP;
+        for (int r = 0; r < RP; ++r) {
+            const float vv = vr[r];
+#pragma unroll
+            for (int l = 0; l < D; ++l) z[l] += vv * Ymix[r * kLd + t * D + l];
+        }
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            float acc = 0.f;
+#pragma unroll
+            for (int l = 0; l < D; ++l) acc += z[l] * P.Jinv[l * D + k];
+            ab[k] = cprod * ab[k] - acc;
+            X[n * kLd + t * D + k] = ab[k];
+        }
+    }
+    __syncthreads();
+    if (valid) eval_exact<D>(P, X + t * D, n, q, v);
+    {
+        WP<D> w;
+        evaluate(q, v, true, w);
+    }
+    __syncthreads();
+    if (tvalid) {
+        const Fin f = finalize();
+        const bool ok = sqrtf(f.a0) < P.eps_p && sqrtf(f.a1) < P.eps_p && sqrtf(f.b0) < P.eps_v &&
+                        sqrtf(f.b1) < P.eps_v && f.tx <= P.pmax && f.tn >= P.pmin && f.va <= P.vmax;
+        st.outer_iterations = 1;
+        st.constraints_ok = ok ? 1 : 0;
+        if (valid) {
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                if (P.traj_out) P.traj_out[(b * N + n) * D + k] = q[k];
+                if (P.alpha_out) P.alpha_out[(b * N + n) * D + k] = ab[k];
+            }
+        }
+        if (P.stats && n == 0) P.stats[b] = st;
+    }
+}
+
 // --------------------------------------------------- α-space eval kernels
 // mode 0: evaluate (K or dK)·α·J; 1: cost; 2: cost + grad; 3: constraints.
 // trajectory.py:63-65, 271-297, 129-180; same lane mapping as k_optimize.
@@ -1443,6 +1863,10 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s) {
     if (grid <= 0) return hipSuccess;
     return dispatch_t(p.BT, [&](auto tc) {
         constexpr int TT = decltype(tc)::value;
+        if constexpr (!Sh::kVariants && TT <= 512) {  // GD single loop: the lean kernel
+            if (p.lean_ok && p.regops && p.optimizer == IRM_OPT_GD && p.max_outer == 1 && !p.record_series)
+                return launch_lds(k_gd_single<Sh, TT>, grid, p.BT, lds, s, p);
+        }
         auto go = [&](auto bc) {
             constexpr bool BB = decltype(bc)::value;
             if constexpr (TT <= 512) {

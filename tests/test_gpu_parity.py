@@ -409,3 +409,34 @@ def test_object_api(g_e2e):
         assert traj.shape == (50, 3)
         g = tr.compute_trajectory_cost_g(alpha, env.obstacles, env.start_config, env.goal_config, 0.5, 0.1, 0.5)
         assert g.shape == (50, 3) and np.all(np.isfinite(g))
+
+
+@pytest.mark.parametrize("N,mode", [(128, "bench"), (128, "faithful"), (50, "faithful"), (256, "bench")])
+def test_lean_gd_kernel_equals_general(N, mode):
+    """k_gd_single (GD single loop, shape-specialised) vs the general k_optimize
+    (IRM_GENERAL_KERNEL=1) on the same problems: same step counts and statistics, waypoints equal
+    up to the rounding of the block-wide dense/sparse stage-1 choice, which the general kernel also
+    makes from trajectories that have already stopped (≤ 1e-5; in practice mostly bit-equal)."""
+    from irm_motion_planning_amd.context import Context
+    argv = ["--optimizer-name", "gd", "--max-outer-iteration", "1", "--n-timesteps", str(N)]
+    if mode == "bench":
+        argv += ["--loop-loss-reduction=-1e30", "--max-inner-iteration", "60"]
+    rng = np.random.default_rng(31)
+    B = 48
+    s = rng.uniform(-0.5, 0.5, (B, 3)).astype(np.float32)
+    g = rng.uniform(0.2, 1.6, (B, 3)).astype(np.float32)
+    lean = Context(params(*argv))
+    os.environ["IRM_GENERAL_KERNEL"] = "1"
+    try:
+        gen = Context(params(*argv))
+    finally:
+        del os.environ["IRM_GENERAL_KERNEL"]
+    a1, t1, st1 = lean.optimize(s, g, obstacles())
+    a2, t2, st2 = gen.optimize(s, g, obstacles())
+    for k in ("inner_iterations", "outer_iterations", "grad_evals", "cost_evals", "constraints_ok"):
+        np.testing.assert_array_equal(st1[k], st2[k], err_msg=k)
+    np.testing.assert_allclose(t1, t2, rtol=0, atol=1e-5)
+    np.testing.assert_allclose(st1["final_loss"], st2["final_loss"], rtol=1e-6)
+    np.testing.assert_array_equal(t1, lean.evaluate(a1))  # traj_out == K·α_out·J exactly
+    print(f"N={N} {mode}: bit-equal trajectories {np.mean(np.all(t1 == t2, axis=(1, 2))):.2f}, "
+          f"max |dT| {np.abs(t1 - t2).max():.2e}")
