@@ -101,6 +101,16 @@ def flops_per_iteration(N, D, O, R):
     return exec_f, ref_f
 
 
+def optimiser_kernel(a, info, N, D, opt, B):
+    """Which optimiser kernel the launch uses (mirrors launch_optimize_shape's dispatch)."""
+    tb = a.tb or min(info["traj_per_block"], -(-B // info["num_cus"]))
+    nw = -(-N // 64) * 64
+    lean = (opt == "gd" and not a.faithful and (D, N) in ((3, 50), (3, 64), (3, 128), (3, 256), (7, 256))
+            and info["operator_rank"] == 32 and tb * nw <= 512 and N <= 128)
+    return ("irm::k_gd_single (GD single loop; fp32 MFMA 16x16x4 + VALU)" if lean
+            else "irm::k_optimize (fp32 MFMA 16x16x4 + VALU)")
+
+
 def cpu_baseline(cfg, args, start, goal, obstacles, budget_s=12.0):
     """Oracle (C restatement of the reference, OpenMP over trajectories) on a bounded sample."""
     from irm_motion_planning_amd.params import params_from_args
@@ -124,7 +134,7 @@ def cpu_baseline(cfg, args, start, goal, obstacles, budget_s=12.0):
 
 
 def pmc_traffic(cfg):
-    """HBM bytes per k_optimize launch from the newest profiles/*_pmc.json (rocprofv3 FETCH_SIZE /
+    """HBM bytes per optimiser launch from the newest profiles/*_pmc.json (rocprofv3 FETCH_SIZE /
     WRITE_SIZE passes of this bench command, tools/profile_round.sh), or None."""
     import glob
     files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc.json")))
@@ -267,7 +277,7 @@ def main():
             "frac": ref_tflops / PEAK_FP32_TFLOPS,
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel": "irm::k_optimize (fp32 MFMA 16x16x4 + VALU)",
+            "kernel": optimiser_kernel(a, info, N, D, opt, B),
             "kernel_ms": kernel_ms,
             "algorithmic_flops_per_iteration": ref_f,
             "executed_flops_per_iteration": exec_f,

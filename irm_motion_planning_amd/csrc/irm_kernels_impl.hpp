@@ -1319,7 +1319,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
 // (done, b' non-zero away from the endpoints) are read by every wave after the end
 // barrier.  Shape-specialised, operators register-resident (REGOPS) only.
 template <class S, int MAXT>
-__global__ __launch_bounds__(MAXT) void k_gd_single(KParams P) {
+__global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams P) {
     constexpr int D = S::D;
     constexpr int S1Q = kS1Q(MAXT), S2T = kS2T(MAXT);
     constexpr bool RV = MAXT > 256;  // velocity half of stage 1 register-resident too
@@ -1341,6 +1341,8 @@ __global__ __launch_bounds__(MAXT) void k_gd_single(KParams P) {
     const bool valid = tvalid && n < N;
     const bool yrow = tvalid && n < RP;
     const size_t b = (size_t)(tb0 + (tvalid ? t : 0));
+    Prof prof;
+    if (tid == 0) prof.init();
 
     float* X = smem + H.X;
     float* dP = smem + H.dP;
@@ -1404,6 +1406,7 @@ __global__ __launch_bounds__(MAXT) void k_gd_single(KParams P) {
     // evaluation of (q2, v2) with this trajectory's waves: wave partials + endpoint rows
     auto evaluate = [&](const float (&q2)[D], const float (&v2)[D], bool ext, WP<D>& w) {
         if (valid) eval_waypoint<D>(P, q2, v2, obs, w);
+        IRM_STAMP(6);
         const float us = P.one_m_lmax * (w.cv * P.invN) + ljl * ((w.jp + w.jv) * P.invN);
         ered_store(valid, w.cv, us, w.tx, w.tn, w.va, ext, n0, red, wave);
         if (valid && (n == 0 || n == N - 1)) {  // trajectory.py:183-204 rows 0 and N−1
@@ -1552,6 +1555,7 @@ __global__ __launch_bounds__(MAXT) void k_gd_single(KParams P) {
     }
     __syncthreads();
 
+    IRM_STAMP(14);
     // ---------------------------------------------------------- GD rounds
     int inner = 0;
     float cprod = 1.f;
@@ -1576,8 +1580,12 @@ __global__ __launch_bounds__(MAXT) void k_gd_single(KParams P) {
                 e1[k] = X[(NK + N - 1) * kLd + t * D + k];
             }
         }
+        IRM_STAMP(0);
+        IRM_COUNT(13, dense);
         stage1(dense);
+        IRM_STAMP(1);
         __syncthreads();
+        IRM_STAMP(2);
         {  // stage 2: dP = F·Σ_s Ypart[s]
             const float* xl = Ypart + (lane >> 4) * kLd + (lane & 15);
             f32x4 acc[S2T];
@@ -1615,7 +1623,9 @@ __global__ __launch_bounds__(MAXT) void k_gd_single(KParams P) {
             for (int j = 0; j < S2T; ++j)
                 if (wave + j * nwaves < MT2) store_tile(dP, wave + j * nwaves, acc[j], 0xFFFFu);
         }
+        IRM_STAMP(3);
         __syncthreads();
+        IRM_STAMP(4);
         float q2[D], v2[D];
         WP<D> w;
         if (!done) {  // wave-uniform
@@ -1631,11 +1641,15 @@ __global__ __launch_bounds__(MAXT) void k_gd_single(KParams P) {
                 q2[k] = cfac * q[k] - step * ut;
                 v2[k] = cfac * v[k] - step * uv;
             }
+            IRM_STAMP(5);
             evaluate(q2, v2, false, w);
         }
+        IRM_STAMP(7);
         __syncthreads();
+        IRM_STAMP(8);
         if (!done) {
             const Fin f = finalize();
+            IRM_STAMP(9);
             st.grad_evals++;
             st.cost_evals++;
             bool bfar = false;
@@ -1658,7 +1672,9 @@ __global__ __launch_bounds__(MAXT) void k_gd_single(KParams P) {
             }
             if (lane == 0) wflag[wave] = (done ? 1u : 0u) | (bfar ? 2u : 0u);
         }
+        IRM_STAMP(11);
         __syncthreads();
+        IRM_STAMP(12);
     }
 
     // ---------------------------------------------------------- epilogue
@@ -1725,6 +1741,7 @@ __global__ __launch_bounds__(MAXT) void k_gd_single(KParams P) {
         }
         if (P.stats && n == 0) P.stats[b] = st;
     }
+    if (tid == 0) prof.flush(P.prof);
 }
 
 // --------------------------------------------------- α-space eval kernels

@@ -23,6 +23,12 @@ PHASES = ["dir:stage1 barrier-wait", "dir: latch + endpoint reads", "dir:y rows 
           "finalize: partial reads"]
 
 
+LEAN_PHASES = ["round top: flags + latch reads", "stage-1 MFMA", "stage-1 barrier wait", "stage 2",
+               "stage-2 barrier wait", "dP latch + update", "eval_waypoint", "reductions + endpoint rows",
+               "E1 barrier wait", "finalize", "(unused)", "decide + grad inputs", "end barrier wait",
+               "#rounds with dense stage 1 (count)", "prologue"] + ["(unused)"] * 9
+
+
 def run(cfg, tb=0, rank=0, faithful=False):
     args = bench.make_args(cfg, faithful, 200)
     start, goal, obstacles = bench.make_problem(cfg, 1, 0)
@@ -41,7 +47,7 @@ def run(cfg, tb=0, rank=0, faithful=False):
     tot = prof.sum(1) - prof[:, 13]
     print(f"== {cfg} tb={info['traj_per_block']} R={info['operator_rank']} blocks={n} host {1000*dt:.2f} ms "
           f"rounds~{rounds:.0f} total cycles/block mean {tot.mean():.0f} -> {tot.mean()/rounds:.0f} per round")
-    for i, name in enumerate(PHASES):
+    for i, name in enumerate(LEAN_PHASES if os.environ.get("IRM_PROFILE_LEAN") else PHASES):
         c = prof[:, i].mean()
         if i == 13:
             print(f"   {name:22s} {c:9.1f} of {rounds:.0f} rounds")

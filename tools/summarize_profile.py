@@ -1,7 +1,7 @@
 """Condense a tools/profile_round.sh run into profiles/<round>_*.
 
 profiles/<round>_kernel_stats.csv  rocprofv3 --stats table (as produced)
-profiles/<round>_pmc.json          per-dispatch FETCH_SIZE / WRITE_SIZE of k_optimize and the
+profiles/<round>_pmc.json          per-dispatch FETCH_SIZE / WRITE_SIZE of the optimiser kernel and the
                                    corrected HBM bytes (MI355X_MICROARCH.md §HBM: FETCH_SIZE
                                    counts half the bytes of wide streaming reads on gfx950 → ×2)
 bench.py reads the newest *_pmc.json for roofline.traffic.
@@ -21,11 +21,11 @@ def find(d, pattern):
     return hits[0] if hits else None
 
 
-def counter_rows(path, kernel_sub="k_optimize"):
+def counter_rows(path, kernel_subs=("k_gd_single", "k_optimize")):
     vals = {}
     with open(path) as f:
         for row in csv.DictReader(f):
-            if kernel_sub not in row.get("Kernel_Name", ""):
+            if not any(k in row.get("Kernel_Name", "") for k in kernel_subs):
                 continue
             key = row.get("Dispatch_Id") or row.get("Correlation_Id")
             vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
@@ -39,7 +39,7 @@ def main():
     stats = find(os.path.join(out, "stats"), "*kernel_stats.csv")
     if stats:
         shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    res = {"round": tag, "kernel": "irm::k_optimize", "command": "python bench.py --no-cpu-baseline --steps 5 --warmup 1"}
+    res = {"round": tag, "kernel": "irm::k_gd_single / irm::k_optimize (the optimiser launch)", "command": "python bench.py --no-cpu-baseline --steps 5 --warmup 1"}
     for name, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
         path = find(os.path.join(out, sub), "*counter_collection.csv")
         if not path:
