@@ -38,6 +38,8 @@ CONFIGS = {
     # diagnostic shapes (not BASELINE configurations): C3's batch at other trajectory lengths
     "c3n64": ("diagnostic: C3 batch at N=64", 1024, 64, 3, 11, "gd"),
     "c3n256": ("diagnostic: C3 batch at N=256", 1024, 256, 3, 11, "gd"),
+    "c3o0": ("diagnostic: C3 batch without obstacles", 1024, 128, 3, 0, "gd"),
+    "c3o44": ("diagnostic: C3 batch, the reference's obstacles ×4 (shifted copies)", 1024, 128, 3, 44, "gd"),
 }
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X fp32 (vector = matrix), MI355X_MICROARCH.md
@@ -60,6 +62,9 @@ def make_problem(cfg, world, rank):
     else:  # c3, c5, c2 and the diagnostic c3n* shapes
         from irm_motion_planning_amd.environment import OBSTACLES
         obstacles = OBSTACLES[:O].astype(np.float32)
+        if O > len(OBSTACLES):  # diagnostic: shifted copies of the reference set
+            reps = -(-O // len(OBSTACLES))
+            obstacles = np.concatenate([OBSTACLES + 0.1 * i for i in range(reps)])[:O].astype(np.float32)
         rs = np.random.default_rng(4 if cfg == "c5" else 1)
     start = rs.uniform(-0.5, 0.5, (Btot, D)).astype(np.float32)
     goal = rs.uniform(0.2, 1.6, (Btot, D)).astype(np.float32)

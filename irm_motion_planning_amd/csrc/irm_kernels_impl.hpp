@@ -1350,7 +1350,10 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
     float* Ymix = smem + H.Ymix;
     float* red = smem + H.red;
     float* sg = smem + H.sg;
-    unsigned* wflag = reinterpret_cast<unsigned*>(smem + H.wp);  // per wave: bit 0 done, bit 1 b' far
+    // flag words by round parity: bit w = wave w still stepping, bit 31 = some b' non-zero away
+    // from the endpoints (dense stage 1); OR-ed in by lane 0 of each wave, read by all after the
+    // end barrier, the other parity cleared at the round top
+    unsigned* fw = reinterpret_cast<unsigned*>(smem + H.flags);
     float* obsL = smem + H.obs;
 
     const int KQ1 = MP / 16, KQa = NK / 16, MT1 = RP / 16, KQ2 = RP / 16, MT2 = MP / 16;
@@ -1386,6 +1389,7 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
     const float h0V = valid ? P.Hend[NK + n] : 0.f, h1V = valid ? P.Hend[MP + NK + n] : 0.f;
     stage_obstacles(P, tb0, ntb, obsL);
     stage_alpha<D>(P, tb0, ntb, X, NK);
+    if (tid < 2) fw[tid] = 0u;
     __syncthreads();
     float q[D], v[D], s[D], g[D], ab[D], dra[D], drb[D], aca[D], acb[D];
 #pragma unroll
@@ -1551,7 +1555,7 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
         st.cost_evals = 1;
         if (P.max_inner <= 0) done = true;
         const bool bfar = grad_inputs(w, q, v, f.idx);
-        if (lane == 0) wflag[wave] = (done ? 1u : 0u) | (bfar ? 2u : 0u);
+        if (lane == 0 && (!done || bfar)) atomicOr(&fw[0], (done ? 0u : 1u << wave) | (bfar ? 1u << 31 : 0u));
     }
     __syncthreads();
 
@@ -1559,15 +1563,11 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
     // ---------------------------------------------------------- GD rounds
     int inner = 0;
     float cprod = 1.f;
-    for (;;) {
-        unsigned fl = 0xFFFFFFFFu, any = 0u;
-        for (int w2 = 0; w2 < nwaves; ++w2) {
-            const unsigned x = wflag[w2];
-            fl &= x;
-            any |= x;
-        }
-        if (fl & 1u) break;  // every trajectory of the block is done
-        const bool dense = (any & 2u) != 0u;
+    for (int par = 0;; par ^= 1) {
+        const unsigned fl = fw[par];
+        if ((fl & 0x7FFFFFFFu) == 0u) break;  // every trajectory of the block is done
+        const bool dense = (fl >> 31) != 0u;
+        if (tid == 0) fw[par ^ 1] = 0u;
         // this lane's gradient-input rows (α recovery) and the endpoint velocity rows
         float e0[D], e1[D], xa[D], xb[D];
         {
@@ -1670,7 +1670,8 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
                 if (inner >= P.max_inner) done = true;
                 else bfar = grad_inputs(w, q2, v2, f.idx);
             }
-            if (lane == 0) wflag[wave] = (done ? 1u : 0u) | (bfar ? 2u : 0u);
+            if (lane == 0 && (!done || bfar))
+                atomicOr(&fw[par ^ 1], (done ? 0u : 1u << wave) | (bfar ? 1u << 31 : 0u));
         }
         IRM_STAMP(11);
         __syncthreads();
