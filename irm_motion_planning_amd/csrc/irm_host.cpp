@@ -150,10 +150,12 @@ double erfinv_f64(double y) {
     return x;
 }
 
-void fill_frag(std::vector<float>& out, int M, int K, const std::vector<double>& A /*row-major M×K*/) {
+void fill_frag(std::vector<float>& out, int M, int K, const std::vector<double>& A /*row-major M×K*/,
+               bool kperm = false) {
     out.assign((size_t)irm::frag_floats(M, K), 0.f);
     for (int r = 0; r < M; ++r)
-        for (int k = 0; k < K; ++k) out[(size_t)irm::frag_index(r, k, K)] = (float)A[(size_t)r * K + k];
+        for (int k = 0; k < K; ++k)
+            out[(size_t)(kperm ? irm::frag_index_kp(r, k, K) : irm::frag_index(r, k, K))] = (float)A[(size_t)r * K + k];
 }
 
 int round_up(int x, int m) { return (x + m - 1) / m * m; }
@@ -169,7 +171,7 @@ struct irm_ctx {
     KParams kp{};
     // device
     float *d_K = nullptr, *d_dK = nullptr, *d_Kt = nullptr, *d_dKt = nullptr, *d_F1 = nullptr, *d_F2 = nullptr,
-          *d_Fbot = nullptr, *d_Vr = nullptr, *d_H = nullptr, *d_u = nullptr, *d_w = nullptr;
+          *d_F1p = nullptr, *d_F2p = nullptr, *d_Fbot = nullptr, *d_Vr = nullptr, *d_H = nullptr, *d_u = nullptr, *d_w = nullptr;
     // host-API staging
     void* d_io = nullptr;
     size_t io_bytes = 0;
@@ -463,11 +465,15 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
         for (int r = 0; r < RP; ++r) A[(size_t)r * MP + frow(m)] = F[(size_t)m * RP + r];
     fill_frag(frag, RP, MP, A);
     rc |= upload(&c->d_F1, frag);
+    fill_frag(frag, RP, MP, A, true);
+    rc |= upload(&c->d_F1p, frag);
     A.assign((size_t)MP * RP, 0.0);  // F (MP × RP)
     for (int m = 0; m < 2 * N; ++m)
         for (int r = 0; r < RP; ++r) A[(size_t)frow(m) * RP + r] = F[(size_t)m * RP + r];
     fill_frag(frag, MP, RP, A);
     rc |= upload(&c->d_F2, frag);
+    fill_frag(frag, MP, RP, A, true);
+    rc |= upload(&c->d_F2p, frag);
     std::vector<float> fb((size_t)N * RP), vr((size_t)N * RP);
     for (int n = 0; n < N; ++n)
         for (int r = 0; r < RP; ++r) {
@@ -624,6 +630,8 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
     kp.dKt = c->d_dKt;
     kp.F1frag = c->d_F1;
     kp.F2frag = c->d_F2;
+    kp.F1p = c->d_F1p;
+    kp.F2p = c->d_F2p;
     kp.Fbot = c->d_Fbot;
     kp.Vr = c->d_Vr;
     kp.Hend = c->d_H;
@@ -661,7 +669,7 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
 void irm_ctx_destroy(irm_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->p.device);
-    float* bufs[] = {c->d_K, c->d_dK, c->d_Kt, c->d_dKt, c->d_F1,   c->d_F2,
+    float* bufs[] = {c->d_K, c->d_dK, c->d_Kt, c->d_dKt, c->d_F1,   c->d_F2, c->d_F1p, c->d_F2p,
                      c->d_Fbot, c->d_Vr, c->d_H, c->d_u, c->d_w};
     for (float* b : bufs)
         if (b) (void)hipFree(b);

@@ -61,6 +61,8 @@ struct KParams {
     const float* dKt;     // dKᵀ, row-major               (N × N)
     const float* F1frag;  // A-fragments of Fᵀ            (RP × MP)
     const float* F2frag;  // A-fragments of F             (MP × RP)
+    const float* F1p;     // Fᵀ / F in the k-permuted fragment layout (frag_index_kp) of the
+    const float* F2p;     //   lean kernel, whose B operands are 4 consecutive rows per lane
     const float* Fbot;    // F rows N..2N-1, row-major    (N × RP)
     const float* Vr;      // V_R, row-major               (N × RP)
     const float* Hend;    // F·F[NK]ᵀ, F·F[NK+N−1]ᵀ: operator columns of the endpoint velocity rows (2 × MP)
@@ -99,6 +101,15 @@ __host__ __device__ inline int64_t frag_index(int row, int k, int K) {
     int KQ = (K + 15) / 16;
     int mt = row / 16, kq = k / 16, kk = k % 16;
     int lane = (row % 16) + 16 * (kk % 4), j = kk / 4;
+    return (((int64_t)mt * KQ + kq) * 64 + lane) * 4 + j;
+}
+
+// k-permuted variant: MFMA j of k-group kq takes k = 16·kq + 4·(lane>>4) + j, so a lane's four
+// B values of a k-group are 4 consecutive rows (one ds_read_b128 from a column-major buffer).
+__host__ __device__ inline int64_t frag_index_kp(int row, int k, int K) {
+    int KQ = (K + 15) / 16;
+    int mt = row / 16, kq = k / 16, kk = k % 16;
+    int lane = (row % 16) + 16 * (kk / 4), j = kk % 4;
     return (((int64_t)mt * KQ + kq) * 64 + lane) * 4 + j;
 }
 
@@ -144,7 +155,7 @@ __host__ __device__ constexpr Head plan_head(int MP, int RP, int nsplit, bool op
     H.Ypart = H.Ymix = 0;
     if (optimizer) {
         H.Ypart = off;
-        off += al4(nsplit * RP * kLd);
+        off += al4(nsplit * (RP * kLd > 16 * (RP + 8) ? RP * kLd : 16 * (RP + 8)));
         H.Ymix = off;
         off += al4(RP * kLd);
     }

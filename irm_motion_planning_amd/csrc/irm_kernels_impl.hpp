@@ -1318,6 +1318,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
 // phase logic, no direction / resync masks and no LDS atomics — per-wave flag words
 // (done, b' non-zero away from the endpoints) are read by every wave after the end
 // barrier.  Shape-specialised, operators register-resident (REGOPS) only.
+// LDS is column-major here — X / dP as [column][row] (stride MP + 8), the stage-1 partials as
+// [split][column][r] (stride RP + 8) — with the k-permuted operator fragments (F1p / F2p,
+// frag_index_kp): a lane's four B values of a k-group are then one ds_read_b128 and an MFMA
+// result tile one ds_write_b128 per lane (strides ≡ 8 mod 16 keep both conflict-free).
 template <class S, int MAXT>
 __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams P) {
     constexpr int D = S::D;
@@ -1358,6 +1362,8 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
 
     const int KQ1 = MP / 16, KQa = NK / 16, MT1 = RP / 16, KQ2 = RP / 16, MT2 = MP / 16;
     const int nsplit = sh.NSPLIT;
+    const int ldx = MP + 8, ldy = RP + 8;  // column strides of X / dP and of the stage-1 partials
+    const int cl = lane & 15, r4 = 4 * (lane >> 4);  // MFMA column / first of 4 rows of this lane
     const bool has1 = wave < MT1 * nsplit;
     const int tile1 = wave % MT1, sp1 = wave / MT1;
     const int kq0 = (KQa * sp1) / nsplit, kq1 = (KQa * (sp1 + 1)) / nsplit;
@@ -1365,8 +1371,8 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
     // ----------------------------------------------------------- prologue
     f32x4 a1[S1Q], a1v[RV ? S1Q : 1], a2[S2T * 2];
     {
-        const f32x4* g1 = reinterpret_cast<const f32x4*>(P.F1frag);
-        const f32x4* g2 = reinterpret_cast<const f32x4*>(P.F2frag);
+        const f32x4* g1 = reinterpret_cast<const f32x4*>(P.F1p);
+        const f32x4* g2 = reinterpret_cast<const f32x4*>(P.F2p);
 #pragma unroll
         for (int i = 0; i < S1Q; ++i) {
             a1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1471,8 +1477,8 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
                     ma += a[d] * P.JtJ[d * D + k];
                     mb += bb[d] * P.JtJ[d * D + k];
                 }
-                X[n * kLd + t * D + k] = ma;
-                X[(NK + n) * kLd + t * D + k] = mb;
+                X[(t * D + k) * ldx + n] = ma;
+                X[(t * D + k) * ldx + NK + n] = mb;
                 bfar |= (!endrow && bb[k] != 0.f);
             }
         }
@@ -1480,32 +1486,23 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
     };
     auto stage1 = [&](bool full) {  // Ypart[sp] = Fᵀ·[a'; b'] over this wave's unit
         if (!has1) return;
-        const float* xl = X + (lane >> 4) * kLd + (lane & 15);
+        const float* xl = X + cl * ldx + r4;
         constexpr bool kFix = S::KQU > 0 && S::KQU <= S1Q;
         constexpr int KQU = kFix ? S::KQU : S1Q;
         auto in = [&](int i) { return kFix ? i < KQU : kq0 + i < kq1; };
-        float bv[KQU][4], bw[RV ? KQU : 1][4];
+        const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+        f32x4 bv[KQU], bw[RV ? KQU : 1];
 #pragma unroll
-        for (int i = 0; i < KQU; ++i) {
-            const float* xb = xl + (kq0 + i) * 16 * kLd;
-            bv[i][0] = in(i) ? xb[0] : 0.f;
-            bv[i][1] = in(i) ? xb[4 * kLd] : 0.f;
-            bv[i][2] = in(i) ? xb[8 * kLd] : 0.f;
-            bv[i][3] = in(i) ? xb[12 * kLd] : 0.f;
-        }
+        for (int i = 0; i < KQU; ++i)
+            bv[i] = in(i) ? *reinterpret_cast<const f32x4*>(xl + (kq0 + i) * 16) : z4;
         if constexpr (RV) {
             if (full) {
 #pragma unroll
-                for (int i = 0; i < KQU; ++i) {
-                    const float* xb = xl + (KQa + kq0 + i) * 16 * kLd;
-                    bw[i][0] = in(i) ? xb[0] : 0.f;
-                    bw[i][1] = in(i) ? xb[4 * kLd] : 0.f;
-                    bw[i][2] = in(i) ? xb[8 * kLd] : 0.f;
-                    bw[i][3] = in(i) ? xb[12 * kLd] : 0.f;
-                }
+                for (int i = 0; i < KQU; ++i)
+                    bw[i] = in(i) ? *reinterpret_cast<const f32x4*>(xl + (KQa + kq0 + i) * 16) : z4;
             }
         }
-        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        f32x4 acc0 = z4, acc1 = z4;
 #pragma unroll
         for (int i = 0; i < KQU; ++i) {
             if (in(i)) {
@@ -1527,19 +1524,18 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
                     }
                 }
             } else {
-                const f32x4* ap = reinterpret_cast<const f32x4*>(P.F1frag) + ((size_t)tile1 * KQ1 + KQa) * 64 + lane;
+                const f32x4* ap = reinterpret_cast<const f32x4*>(P.F1p) + ((size_t)tile1 * KQ1 + KQa) * 64 + lane;
                 for (int kq = kq0; kq < kq1; ++kq) {
                     const f32x4 a = ap[(size_t)kq * 64];
-                    const float* xb = xl + (KQa + kq) * 16 * kLd;
-                    const float b0 = xb[0], b1 = xb[4 * kLd], b2 = xb[8 * kLd], b3 = xb[12 * kLd];
-                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b0, acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b1, acc1, 0, 0, 0);
-                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b2, acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b3, acc1, 0, 0, 0);
+                    const f32x4 bb = *reinterpret_cast<const f32x4*>(xl + (KQa + kq) * 16);
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], bb[0], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], bb[1], acc1, 0, 0, 0);
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], bb[2], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], bb[3], acc1, 0, 0, 0);
                 }
             }
         }
-        store_tile(Ypart + sp1 * RP * kLd, tile1, acc0 + acc1, 0xFFFFu);
+        *reinterpret_cast<f32x4*>(Ypart + (sp1 * 16 + cl) * ldy + tile1 * 16 + r4) = acc0 + acc1;
     };
 
     // round 0 (optimizer_GD.py:295: the loss at α0) and the first gradient inputs
@@ -1574,10 +1570,11 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
             const int nr = valid ? n : 0;
 #pragma unroll
             for (int k = 0; k < D; ++k) {
-                xa[k] = X[nr * kLd + t * D + k];
-                xb[k] = X[(NK + nr) * kLd + t * D + k];
-                e0[k] = X[NK * kLd + t * D + k];
-                e1[k] = X[(NK + N - 1) * kLd + t * D + k];
+                const float* xc = X + (t * D + k) * ldx;
+                xa[k] = xc[nr];
+                xb[k] = xc[NK + nr];
+                e0[k] = xc[NK];
+                e1[k] = xc[NK + N - 1];
             }
         }
         IRM_STAMP(0);
@@ -1587,22 +1584,16 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
         __syncthreads();
         IRM_STAMP(2);
         {  // stage 2: dP = F·Σ_s Ypart[s]
-            const float* xl = Ypart + (lane >> 4) * kLd + (lane & 15);
             f32x4 acc[S2T];
 #pragma unroll
             for (int j = 0; j < S2T; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-            float bv[2][4];
+            f32x4 bv[2];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                bv[i][0] = bv[i][1] = bv[i][2] = bv[i][3] = 0.f;
+                bv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
                 if (i < KQ2) {
-                    for (int sp = 0; sp < nsplit; ++sp) {
-                        const float* x = xl + (sp * RP + i * 16) * kLd;
-                        bv[i][0] += x[0];
-                        bv[i][1] += x[4 * kLd];
-                        bv[i][2] += x[8 * kLd];
-                        bv[i][3] += x[12 * kLd];
-                    }
+                    for (int sp = 0; sp < nsplit; ++sp)
+                        bv[i] += *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + cl) * ldy + i * 16 + r4);
                 }
             }
 #pragma unroll
@@ -1621,7 +1612,8 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
             }
 #pragma unroll
             for (int j = 0; j < S2T; ++j)
-                if (wave + j * nwaves < MT2) store_tile(dP, wave + j * nwaves, acc[j], 0xFFFFu);
+                if (wave + j * nwaves < MT2)
+                    *reinterpret_cast<f32x4*>(dP + cl * ldx + (wave + j * nwaves) * 16 + r4) = acc[j];
         }
         IRM_STAMP(3);
         __syncthreads();
@@ -1631,7 +1623,7 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
         if (!done) {  // wave-uniform
 #pragma unroll
             for (int k = 0; k < D; ++k) {
-                float ut = dP[n * kLd + t * D + k], uv = dP[(NK + n) * kLd + t * D + k];
+                float ut = dP[(t * D + k) * ldx + n], uv = dP[(t * D + k) * ldx + NK + n];
                 if (!dense) {
                     ut = fmaf(h0T, e0[k], fmaf(h1T, e1[k], ut));
                     uv = fmaf(h0V, e0[k], fmaf(h1V, e1[k], uv));
@@ -1685,8 +1677,8 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
     if (valid) {
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-            X[n * kLd + t * D + k] = aca[k];
-            X[(NK + n) * kLd + t * D + k] = acb[k];
+            X[(t * D + k) * ldx + n] = aca[k];
+            X[(t * D + k) * ldx + NK + n] = acb[k];
         }
     }
     __syncthreads();
@@ -1696,7 +1688,7 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
 #pragma unroll
         for (int d = 0; d < D; ++d) {
             float y = 0.f;
-            for (int sp = 0; sp < nsplit; ++sp) y += Ypart[(sp * RP + n) * kLd + t * D + d];
+            for (int sp = 0; sp < nsplit; ++sp) y += Ypart[(sp * 16 + t * D + d) * ldy + n];
             Ymix[n * kLd + t * D + d] = y;
         }
     }
