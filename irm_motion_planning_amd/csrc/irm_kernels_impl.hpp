@@ -557,8 +557,19 @@ __device__ __forceinline__ void ered_store(bool live, float cv, float us, float 
     s += dppf<0x141>(s);
     m = fmaxf(m, dppf<0x140>(m));
     s += dppf<0x140>(s);
-    const float wm = fmaxf(fmaxf(lanef(m, 0), lanef(m, 16)), fmaxf(lanef(m, 32), lanef(m, 48)));
-    const float ws = (lanef(s, 0) + lanef(s, 16)) + (lanef(s, 32) + lanef(s, 48));
+    // cross-row combine with the CDNA4 row / half swaps: (r0 ∘ r1) ∘ (r2 ∘ r3) in every lane, the
+    // association of the readlane form (lanes 0, 16, 32, 48)
+    float wm, ws;
+    {
+        auto pm = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+        auto ps = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+        const float m2 = fmaxf(__uint_as_float(pm[0]), __uint_as_float(pm[1]));
+        const float s2 = __uint_as_float(ps[0]) + __uint_as_float(ps[1]);
+        auto qm = __builtin_amdgcn_permlane32_swap(__float_as_uint(m2), __float_as_uint(m2), false, false);
+        auto qs = __builtin_amdgcn_permlane32_swap(__float_as_uint(s2), __float_as_uint(s2), false, false);
+        wm = fmaxf(__uint_as_float(qm[0]), __uint_as_float(qm[1]));
+        ws = __uint_as_float(qs[0]) + __uint_as_float(qs[1]);
+    }
     const unsigned long long hit = __ballot(live && cv == wm);
     const int idx = hit ? n0 + __builtin_ctzll(hit) : 0x7fffffff;
     float ox = 0.f, on = 0.f, oa = 0.f;
@@ -1479,7 +1490,7 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
                 }
                 X[(t * D + k) * ldx + n] = ma;
                 X[(t * D + k) * ldx + NK + n] = mb;
-                bfar |= (!endrow && bb[k] != 0.f);
+                bfar |= (bb[k] != 0.f) & !endrow;  // branch-free
             }
         }
         return __ballot(bfar) != 0ull;
