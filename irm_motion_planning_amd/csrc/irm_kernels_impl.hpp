@@ -220,27 +220,28 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
     // obstacles accumulate separately and are added at the end.
     const f32x4* o4 = reinterpret_cast<const f32x4*>(ob);
     const int nq = (P.O + 3) >> 2;
+    // Per pair of obstacles: e = 1 + dx² + dy² (= 2·den), u = rcp(e); the potential's constants are
+    // applied once at the end: cost = 0.8/den = 1.6·Σu, ∂cost/∂f = −0.8·d/den² = −3.2·Σ d·u².
     auto potential = [&](float x, float y, float& cv, float& ax, float& ay) {
         f32x2 cv2 = {0.f, 0.f}, ax2 = {0.f, 0.f}, ay2 = {0.f, 0.f};
-        const f32x2 fx2 = {x, x}, fy2 = {y, y};
+        const f32x2 fx2 = {x, x}, fy2 = {y, y}, one = {1.f, 1.f};
         auto pair2 = [&](f32x2 ox, f32x2 oy) {
             const f32x2 dx = fx2 - ox, dy = fy2 - oy;
-            const f32x2 r2 = dx * dx + dy * dy;
-            const f32x2 den = 0.5f + 0.5f * r2;
-            const f32x2 inv = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
-            cv2 += 0.8f * inv;
-            const f32x2 i2 = inv * inv;
-            ax2 += (-0.8f * dx) * i2;
-            ay2 += (-0.8f * dy) * i2;
+            const f32x2 e = dy * dy + (dx * dx + one);
+            const f32x2 u = {__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
+            cv2 += u;
+            const f32x2 u2 = u * u;
+            ax2 += dx * u2;
+            ay2 += dy * u2;
         };
         for (int c = 0; c < nq; ++c) {
             const f32x4 p0 = o4[2 * c], p1 = o4[2 * c + 1];
             pair2(p0.xy, p0.zw);
             pair2(p1.xy, p1.zw);
         }
-        cv = cv2.x + cv2.y;
-        ax = ax2.x + ax2.y;
-        ay = ay2.x + ay2.y;
+        cv = 1.6f * (cv2.x + cv2.y);
+        ax = -3.2f * (ax2.x + ax2.y);
+        ay = -3.2f * (ay2.x + ay2.y);
     };
     if constexpr (!WHOLE) {
         float Cx = 0.f, Cy = 0.f;
