@@ -291,6 +291,10 @@ def main():
             "hbm_algorithmic_bytes_per_launch": bytes_launch,
             "hbm_achieved_gbs": bytes_launch / (kernel_ms * 1e-3) / 1e9,
             "hbm_frac": bytes_launch / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+            "note": "achieved/frac count SURVEY.md 8d's algorithmic flops of the reference's dense alpha-space "
+                    "formulation; the kernel reaches the same iterate with the rank-R trajectory-space operator "
+                    "(executed_flops_per_iteration), so frac > 1 is algorithmic saving and executed_frac is the "
+                    "arithmetic-unit utilisation (DESIGN.md 5)",
         },
         "cpu_baseline": None,
         "iterations_per_step": iters_all,
