@@ -449,3 +449,40 @@ def test_lean_gd_kernel_matches_general(N, mode):
     np.testing.assert_array_equal(t1, lean.evaluate(a1))  # traj_out == K·α_out·J exactly
     print(f"N={N} {mode}: same step counts {same.mean():.2f}, bit-equal {np.mean(np.all(t1 == t2, axis=(1, 2))):.2f}, "
           f"max |dT| {np.abs(t1[same] - t2[same]).max():.2e}")
+
+
+@pytest.mark.parametrize("N,D,links", [(33, 3, None), (100, 3, None), (96, 4, [1.0, 0.8, 0.6, 0.4]),
+                                       (200, 2, [1.5, 1.0]), (64, 5, [0.8, 0.7, 0.6, 0.5, 0.4])])
+def test_generic_shapes_match_reference_iteration(N, D, links):
+    """Shapes outside the specialised set (k_optimize<DynShape<D>>, odd N, D ≠ 3): 15 GD steps
+    (λmax = 0) vs the reference algorithm in exact arithmetic from the same α0 (oracle/ref64.py),
+    with the band of test_per_problem_obstacles_and_edge_counts (3 × the exact run's ±1-ulp
+    sensitivity + 2 × the α fp32 representation error + 1e-3); the final loss within 1e-3 relative
+    of the exact iteration's (the fp32 α-space iteration of the reference drifts from it by up to
+    1e-3 here: SURVEY.md A.1, tests/test_oracle_golden.py::test_fp32_alpha_drift)."""
+    from conftest import ref_args
+    argv = ["--optimizer-name", "gd", "--max-outer-iteration", "1", "--max-inner-iteration", "15",
+            "--loop-loss-reduction=-1e30", "--lambda-max-cost", "0", "--n-timesteps", str(N),
+            "--n-joints", str(D)]
+    if links:
+        argv += ["--link-length"] + [str(x) for x in links]
+    c = ctx(*argv)
+    o, r = _ref64(ref_args(*argv))
+    rng = np.random.default_rng(N + D)
+    B = 6
+    s = rng.uniform(-0.5, 0.5, (B, D)).astype(np.float32)
+    g = rng.uniform(0.2, 1.6, (B, D)).astype(np.float32)
+    obs = obstacles()
+    _, traj, st = c.optimize(s, g, obs)
+    assert np.all(st["grad_evals"] == 15)
+    for b in range(B):
+        a0 = c.init_alpha(s[b], g[b])
+        T64, l64, _, spread, _ = _ref64_band(r, a0, obs, s[b], g[b], 15)
+        a64, _, _ = r.gd_single(a0, obs, s[b], g[b], 15)
+        rnd = float(np.abs(r.traj_vel(a64.astype(np.float32))[0] - T64).max())
+        err = float(np.abs(traj[b] - T64).max())
+        assert err <= 3 * spread + 2 * rnd + 1e-3, (b, err, spread, rnd)
+        l_hip = float(st["final_loss"][b])
+        print(f"N={N} D={D} b={b}: |dT| {err:.2e} (band {3 * spread + 2 * rnd + 1e-3:.2e}), "
+              f"loss {l_hip:.6f} vs exact {float(l64):.6f}")
+        assert abs(l_hip - float(l64)) <= 1e-3 * abs(float(l64))
