@@ -110,8 +110,11 @@ def optimiser_kernel(a, info, N, D, opt, B):
     """Which optimiser kernel the launch uses (mirrors launch_optimize_shape's dispatch)."""
     tb = a.tb or min(info["traj_per_block"], -(-B // info["num_cus"]))
     nw = -(-N // 64) * 64
+    nk = -(-N // 16) * 16
+    nsplit = (nk // 16 + 3) // 4
+    waves = tb * nw // 64
     lean = (opt == "gd" and not a.faithful and (D, N) in ((3, 50), (3, 64), (3, 128), (3, 256), (7, 256))
-            and info["operator_rank"] == 32 and tb * nw <= 512 and N <= 128)
+            and info["operator_rank"] == 32 and tb * nw <= 512 and 2 * nsplit <= waves)
     return ("irm::k_gd_single (GD single loop; fp32 MFMA 16x16x4 + VALU)" if lean
             else "irm::k_optimize (fp32 MFMA 16x16x4 + VALU)")
 

@@ -1337,7 +1337,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
 template <class S, int MAXT>
 __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams P) {
     constexpr int D = S::D;
-    constexpr int S1Q = kS1Q(MAXT), S2T = kS2T(MAXT);
+    constexpr int S1Q = kS1Q(MAXT);
+    // stage-2 tiles per wave: all of this shape's tiles over the workgroup's waves (N = 256: 4)
+    constexpr int S2T = (S::MP / 16 + MAXT / 64 - 1) / (MAXT / 64) > kS2T(MAXT)
+                            ? (S::MP / 16 + MAXT / 64 - 1) / (MAXT / 64)
+                            : kS2T(MAXT);
     constexpr bool RV = MAXT > 256;  // velocity half of stage 1 register-resident too
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const S sh(P);
@@ -1874,6 +1878,13 @@ struct type_tag {
     using type = T;
 };
 
+// LDS of k_gd_single: the optimiser head + obstacles, no staged operator fragments.
+inline size_t lean_lds(const KParams& p) {
+    KParams q = p;
+    q.regops = 1;
+    return (size_t)plan_lds(q, false, true).total * 4;
+}
+
 // k_optimize<Shape> with the MAXT / operator-placement / optimiser variants (one shape per
 // instantiation unit, irm_opt_inst.hip).
 template <class Sh>
@@ -1886,8 +1897,10 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s) {
     return dispatch_t(p.BT, [&](auto tc) {
         constexpr int TT = decltype(tc)::value;
         if constexpr (!Sh::kVariants && TT <= 512) {  // GD single loop: the lean kernel
-            if (p.lean_ok && p.regops && p.optimizer == IRM_OPT_GD && p.max_outer == 1 && !p.record_series)
-                return launch_lds(k_gd_single<Sh, TT>, grid, p.BT, lds, s, p);
+            // (operators register-resident: one stage-1 unit per wave, enough waves for the units)
+            if (p.lean_ok && p.optimizer == IRM_OPT_GD && p.max_outer == 1 && !p.record_series &&
+                (p.RP / 16) * p.nsplit <= p.BT / 64 && p.NK / 16 <= 4 * p.nsplit)
+                return launch_lds(k_gd_single<Sh, TT>, grid, p.BT, lean_lds(p), s, p);
         }
         auto go = [&](auto bc) {
             constexpr bool BB = decltype(bc)::value;

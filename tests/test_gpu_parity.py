@@ -411,29 +411,33 @@ def test_object_api(g_e2e):
         assert g.shape == (50, 3) and np.all(np.isfinite(g))
 
 
-@pytest.mark.parametrize("N,mode", [(128, "bench"), (128, "faithful"), (50, "faithful"), (256, "bench")])
-def test_lean_gd_kernel_matches_general(N, mode):
+@pytest.mark.parametrize("N,mode,D,tb", [(128, "bench", 3, 0), (128, "faithful", 3, 0), (50, "faithful", 3, 0),
+                                        (256, "bench", 3, 2), (256, "faithful", 3, 2), (256, "bench", 7, 2)])
+def test_lean_gd_kernel_matches_general(N, mode, D, tb):
     """k_gd_single (GD single loop, shape-specialised) vs the general k_optimize
     (IRM_GENERAL_KERNEL=1) on the same problems.  Same algorithm and state; the lean kernel feeds
     the MFMAs k-permuted operators (frag_index_kp), so the 4-term partial sums inside each MFMA
-    group differently.  The fp32 MFMA accumulates exactly like an fmaf chain and the results have
-    been bit-equal on MI355X; the bound allows ulp-level differences that GD would carry along
-    (bench mode, 60 steps: waypoints within 2e-3, final loss within 1e-5 relative).  In
+    group differently.  The fp32 MFMA accumulates exactly like an fmaf chain and for N ≤ 128 the
+    results are bit-equal on MI355X; at N = 256 the general kernel reads its operators from memory
+    in another tiling, and the bound allows the ulp-level differences GD carries along (waypoints
+    within 2e-3, final loss within 2e-4 relative).  In
     faithful mode a trajectory whose last improvement sits within rounding of
     loop_loss_reduction may stop one step earlier or later: at most 10 % of the problems, and
     the others agree as above."""
     from irm_motion_planning_amd.context import Context
-    argv = ["--optimizer-name", "gd", "--max-outer-iteration", "1", "--n-timesteps", str(N)]
+    argv = ["--optimizer-name", "gd", "--max-outer-iteration", "1", "--n-timesteps", str(N), "--n-joints", str(D)]
+    if D != 3:
+        argv += ["--link-length"] + [str(3.0 / D)] * D + ["--gd-lr", "1e-3"]
     if mode == "bench":
         argv += ["--loop-loss-reduction=-1e30", "--max-inner-iteration", "60"]
     rng = np.random.default_rng(31)
     B = 48
-    s = rng.uniform(-0.5, 0.5, (B, 3)).astype(np.float32)
-    g = rng.uniform(0.2, 1.6, (B, 3)).astype(np.float32)
-    lean = Context(params(*argv))
+    s = rng.uniform(-0.5, 0.5, (B, D)).astype(np.float32)
+    g = rng.uniform(0.2, 1.6, (B, D)).astype(np.float32)
+    lean = Context(params(*argv, traj_per_block=tb))
     os.environ["IRM_GENERAL_KERNEL"] = "1"
     try:
-        gen = Context(params(*argv))
+        gen = Context(params(*argv, traj_per_block=tb))
     finally:
         del os.environ["IRM_GENERAL_KERNEL"]
     a1, t1, st1 = lean.optimize(s, g, obstacles())
@@ -445,9 +449,12 @@ def test_lean_gd_kernel_matches_general(N, mode):
     for k in ("outer_iterations",):
         np.testing.assert_array_equal(st1[k], st2[k], err_msg=k)
     np.testing.assert_allclose(t1[same], t2[same], rtol=0, atol=2e-3)
-    np.testing.assert_allclose(st1["final_loss"][same], st2["final_loss"][same], rtol=1e-5)
+    # 2e-4: the λmax > 0 band (a near-tie of two waypoints' costs may pick a different argmax for
+    # one step when the summation differs — at N = 256 the general kernel takes its operators from
+    # memory in another tiling, and 1–2 of 48 problems move by ≤ 1e-4)
+    np.testing.assert_allclose(st1["final_loss"][same], st2["final_loss"][same], rtol=2e-4)
     np.testing.assert_array_equal(t1, lean.evaluate(a1))  # traj_out == K·α_out·J exactly
-    print(f"N={N} {mode}: same step counts {same.mean():.2f}, bit-equal {np.mean(np.all(t1 == t2, axis=(1, 2))):.2f}, "
+    print(f"N={N} D={D} tb={tb} {mode}: same step counts {same.mean():.2f}, bit-equal {np.mean(np.all(t1 == t2, axis=(1, 2))):.2f}, "
           f"max |dT| {np.abs(t1[same] - t2[same]).max():.2e}")
 
 
