@@ -113,9 +113,10 @@ def optimiser_kernel(a, info, N, D, opt, B):
     nk = -(-N // 16) * 16
     nsplit = (nk // 16 + 3) // 4
     waves = tb * nw // 64
+    wpl = 2 if (nw == 256 and 512 < tb * nw <= 1024) else 1  # N = 256, > 2 trajectories: 2 waypoints/lane
     lean = (opt == "gd" and not a.faithful and (D, N) in ((3, 50), (3, 64), (3, 128), (3, 256), (7, 256))
-            and info["operator_rank"] == 32 and tb * nw <= 512 and 2 * nsplit <= waves)
-    return ("irm::k_gd_single (GD single loop; fp32 MFMA 16x16x4 + VALU)" if lean
+            and info["operator_rank"] == 32 and tb * nw // wpl <= 512 and 2 * nsplit <= waves // wpl)
+    return (f"irm::k_gd_single (GD single loop, {wpl} waypoint(s) per lane; fp32 MFMA 16x16x4 + VALU)" if lean
             else "irm::k_optimize (fp32 MFMA 16x16x4 + VALU)")
 
 

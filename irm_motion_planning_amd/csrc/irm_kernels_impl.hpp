@@ -601,6 +601,7 @@ struct FixShape {
     static constexpr int D = D_, N = N_, NK = (N_ + 15) / 16 * 16, MP = 2 * NK, RP = RP_;
     static constexpr int NW = (N_ + 63) / 64 * 64, WPT = NW / 64, NSPLIT = stage1_splits(NK);
     static constexpr bool kVariants = false;  // end-effector cost only (the reference's)
+    static constexpr int kNW = NW;             // lanes per trajectory (0: only known at run time)
     // stage-1 k-quads per split-K unit when the split is even (else 0: checked per quad)
     static constexpr int KQU = (NK / 16) % NSPLIT == 0 ? (NK / 16) / NSPLIT : 0;
     __device__ explicit FixShape(const KParams&) {}
@@ -609,6 +610,7 @@ template <int D_>
 struct DynShape {
     static constexpr int D = D_;
     static constexpr bool kVariants = true;  // cost variants chosen at run time (whole_robot)
+    static constexpr int kNW = 0;
     static constexpr int KQU = 0;
     int N, NK, MP, RP, NW, WPT, NSPLIT;
     __device__ explicit DynShape(const KParams& P)
@@ -1324,17 +1326,79 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
 // optimizer_GD.py:281-310): g = ∇L(α); α' = (1 − λ_reg·lr)·α − lr·g; accept iff
 // L − L(α') ≥ loop_loss_reduction, else stop keeping α; at most max_inner steps; then
 // α is materialised and constraintsFulfilled decides constraints_ok (k_optimize's
-// PH_RESYNC).  The same arithmetic as k_optimize's GD rounds (bit-identical results,
-// tests/test_gpu_parity.py::test_lean_gd_kernel_equals_general) without the general
-// state machine: every trajectory is either stepping or done, so a round needs no
-// phase logic, no direction / resync masks and no LDS atomics — per-wave flag words
-// (done, b' non-zero away from the endpoints) are read by every wave after the end
-// barrier.  Shape-specialised, operators register-resident (REGOPS) only.
+// PH_RESYNC).  The same arithmetic as k_optimize's GD rounds (bit-identical results for
+// N ≤ 128, tests/test_gpu_parity.py::test_lean_gd_kernel_matches_general) without the
+// general state machine: every trajectory is either stepping or done, so a round needs no
+// phase logic, no direction / resync masks; one parity flag word per round (bit per wave
+// still stepping, bit 31 = dense stage 1) is OR-ed by the wave leaders and read by every
+// wave after the end barrier.  Shape-specialised, operators register-resident only.
 // LDS is column-major here — X / dP as [column][row] (stride MP + 8), the stage-1 partials as
 // [split][column][r] (stride RP + 8) — with the k-permuted operator fragments (F1p / F2p,
 // frag_index_kp): a lane's four B values of a k-group are then one ds_read_b128 and an MFMA
 // result tile one ds_write_b128 per lane (strides ≡ 8 mod 16 keep both conflict-free).
-template <class S, int MAXT>
+// WPL waypoints per lane (lane li of a trajectory owns waypoints li + j·NW/WPL): WPL = 2 lets
+// N = 256 trajectories run four to a 512-thread workgroup (C4) without exceeding 256 VGPRs.
+template <int WPL>
+__device__ __forceinline__ void ered_store_wpl(const bool (&live)[WPL], const float (&cv)[WPL], float us,
+                                               float tx, float tn, float va, bool ext, int n0, int nwl,
+                                               float* red, int wave) {
+    if constexpr (WPL == 1) {
+        ered_store(live[0], cv[0], us, tx, tn, va, ext, n0, red, wave);
+    } else {
+        // this lane's best waypoint (first index on ties: j = 0 is the smaller index)
+        float best = live[0] ? cv[0] : -INFINITY;
+        int jb = 0;
+#pragma unroll
+        for (int j = 1; j < WPL; ++j) {
+            const float c = live[j] ? cv[j] : -INFINITY;
+            if (c > best) {
+                best = c;
+                jb = j;
+            }
+        }
+        const bool any = live[0];
+        float m = best, s = any ? us : 0.f;
+        m = fmaxf(m, dppf<0xB1>(m));
+        s += dppf<0xB1>(s);
+        m = fmaxf(m, dppf<0x4E>(m));
+        s += dppf<0x4E>(s);
+        m = fmaxf(m, dppf<0x141>(m));
+        s += dppf<0x141>(s);
+        m = fmaxf(m, dppf<0x140>(m));
+        s += dppf<0x140>(s);
+        auto pm = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+        auto ps = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
+        const float m2 = fmaxf(__uint_as_float(pm[0]), __uint_as_float(pm[1]));
+        const float s2 = __uint_as_float(ps[0]) + __uint_as_float(ps[1]);
+        auto qm = __builtin_amdgcn_permlane32_swap(__float_as_uint(m2), __float_as_uint(m2), false, false);
+        auto qs = __builtin_amdgcn_permlane32_swap(__float_as_uint(s2), __float_as_uint(s2), false, false);
+        const float wm = fmaxf(__uint_as_float(qm[0]), __uint_as_float(qm[1]));
+        const float ws = __uint_as_float(qs[0]) + __uint_as_float(qs[1]);
+        int idx = 0x7fffffff;
+#pragma unroll
+        for (int j = WPL - 1; j >= 0; --j) {  // the smallest j with a hit holds the first index
+            const unsigned long long hit = __ballot(best == wm && jb == j && live[j]);
+            if (hit) idx = n0 + j * nwl + __builtin_ctzll(hit);
+        }
+        float ox = 0.f, on = 0.f, oa = 0.f;
+        if (ext) {
+            ox = wred_max(any ? tx : -INFINITY);
+            on = wred_min(any ? tn : INFINITY);
+            oa = wred_max(any ? va : 0.f);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            float* q = red + wave * 8;
+            q[0] = wm;
+            q[1] = __int_as_float(idx);
+            q[2] = ws;
+            q[3] = ox;
+            q[4] = on;
+            q[5] = oa;
+        }
+    }
+}
+
+template <class S, int MAXT, int WPL>
 __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams P) {
     constexpr int D = S::D;
     constexpr int S1Q = kS1Q(MAXT);
@@ -1343,23 +1407,31 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
                             ? (S::MP / 16 + MAXT / 64 - 1) / (MAXT / 64)
                             : kS2T(MAXT);
     constexpr bool RV = MAXT > 256;  // velocity half of stage 1 register-resident too
+    constexpr int NWL = S::NW / WPL;  // lanes per trajectory
+    constexpr int WPTL = NWL / 64;    // waves per trajectory
+    static_assert(NWL % 64 == 0, "whole waves per trajectory");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const S sh(P);
     const Head H = plan_head(sh.MP, sh.RP, sh.NSPLIT, true);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nwaves = P.BT >> 6;
-    const int N = sh.N, NW = sh.NW, TB = P.TB, RP = sh.RP, MP = sh.MP, NK = sh.NK;
-    const int WPT = sh.WPT;
-    const int t = wave / WPT;
-    const int n = tid - t * NW;
-    const int n0 = (wave - t * WPT) * 64;
+    const int N = sh.N, TB = P.TB, RP = sh.RP, MP = sh.MP, NK = sh.NK;
+    const int t = wave / WPTL;
+    const int li = tid - t * NWL;               // this lane within its trajectory
+    const int n0 = (wave - t * WPTL) * 64;     // li of this wave's lane 0
     const int tb0 = blockIdx.x * TB;
     const int ntb = min(TB, P.B - tb0);
     if (ntb <= 0) return;
     const bool tvalid = t < ntb;
-    const bool valid = tvalid && n < N;
-    const bool yrow = tvalid && n < RP;
+    int nn[WPL];
+    bool vl[WPL];
+#pragma unroll
+    for (int j = 0; j < WPL; ++j) {
+        nn[j] = li + j * NWL;
+        vl[j] = tvalid && nn[j] < N;
+    }
+    const bool yrow = tvalid && li < RP;
     const size_t b = (size_t)(tb0 + (tvalid ? t : 0));
     Prof prof;
     if (tid == 0) prof.init();
@@ -1370,9 +1442,6 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
     float* Ymix = smem + H.Ymix;
     float* red = smem + H.red;
     float* sg = smem + H.sg;
-    // flag words by round parity: bit w = wave w still stepping, bit 31 = some b' non-zero away
-    // from the endpoints (dense stage 1); OR-ed in by lane 0 of each wave, read by all after the
-    // end barrier, the other parity cleared at the round top
     unsigned* fw = reinterpret_cast<unsigned*>(smem + H.flags);
     float* obsL = smem + H.obs;
 
@@ -1407,22 +1476,35 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
                 if (tile < MT2 && i < KQ2) a2[j * 2 + i] = g2[((size_t)tile * KQ2 + i) * 64 + lane];
             }
     }
-    const float h0T = valid ? P.Hend[n] : 0.f, h1T = valid ? P.Hend[MP + n] : 0.f;
-    const float h0V = valid ? P.Hend[NK + n] : 0.f, h1V = valid ? P.Hend[MP + NK + n] : 0.f;
+    float h0T[WPL], h1T[WPL], h0V[WPL], h1V[WPL];
+#pragma unroll
+    for (int j = 0; j < WPL; ++j) {
+        h0T[j] = vl[j] ? P.Hend[nn[j]] : 0.f;
+        h1T[j] = vl[j] ? P.Hend[MP + nn[j]] : 0.f;
+        h0V[j] = vl[j] ? P.Hend[NK + nn[j]] : 0.f;
+        h1V[j] = vl[j] ? P.Hend[MP + NK + nn[j]] : 0.f;
+    }
     stage_obstacles(P, tb0, ntb, obsL);
     stage_alpha<D>(P, tb0, ntb, X, NK);
     if (tid < 2) fw[tid] = 0u;
     __syncthreads();
-    float q[D], v[D], s[D], g[D], ab[D], dra[D], drb[D], aca[D], acb[D];
+    float q[WPL][D], v[WPL][D], ab[WPL][D], dra[WPL][D], drb[WPL][D], aca[WPL][D], acb[WPL][D];
+    float s[D], g[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) {
-        q[k] = v[k] = 0.f;
-        dra[k] = drb[k] = aca[k] = acb[k] = 0.f;
-        ab[k] = valid ? X[n * kLd + t * D + k] : 0.f;
         s[k] = tvalid ? P.start[b * D + k] : 0.f;
         g[k] = tvalid ? P.goal[b * D + k] : 0.f;
     }
-    if (valid) eval_exact<D>(P, X + t * D, n, q, v);  // T0 = (K·α0)·J, V0 = (dK·α0)·J
+#pragma unroll
+    for (int j = 0; j < WPL; ++j) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            q[j][k] = v[j][k] = 0.f;
+            dra[j][k] = drb[j][k] = aca[j][k] = acb[j][k] = 0.f;
+            ab[j][k] = vl[j] ? X[nn[j] * kLd + t * D + k] : 0.f;
+        }
+        if (vl[j]) eval_exact<D>(P, X + t * D, nn[j], q[j], v[j]);  // T0 = (K·α0)·J, V0 = (dK·α0)·J
+    }
     __syncthreads();
     for (int e = tid; e < MP * kLd; e += P.BT) X[e] = 0.f;
     const float* obs = obsL + (P.obs_stride ? t * obs_pitch(P.O) : 0);
@@ -1430,21 +1512,41 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
     const float cfac = 1.f - P.lreg * lr, step = lr;
 
     // evaluation of (q2, v2) with this trajectory's waves: wave partials + endpoint rows
-    auto evaluate = [&](const float (&q2)[D], const float (&v2)[D], bool ext, WP<D>& w) {
-        if (valid) eval_waypoint<D>(P, q2, v2, obs, w);
-        IRM_STAMP(6);
-        const float us = P.one_m_lmax * (w.cv * P.invN) + ljl * ((w.jp + w.jv) * P.invN);
-        ered_store(valid, w.cv, us, w.tx, w.tn, w.va, ext, n0, red, wave);
-        if (valid && (n == 0 || n == N - 1)) {  // trajectory.py:183-204 rows 0 and N−1
-            float a = 0.f, bb = 0.f;
+    auto evaluate = [&](const float (&q2)[WPL][D], const float (&v2)[WPL][D], bool ext, WP<D> (&w)[WPL]) {
+        float cvs[WPL], us = 0.f, tx = -INFINITY, tn = INFINITY, va = 0.f;
 #pragma unroll
-            for (int d = 0; d < D; ++d) {
-                const float e = q2[d] - (n == 0 ? s[d] : g[d]);
-                a += e * e;
-                bb += v2[d] * v2[d];
+        for (int j = 0; j < WPL; ++j) {
+            if (vl[j]) eval_waypoint<D>(P, q2[j], v2[j], obs, w[j]);
+            cvs[j] = w[j].cv;
+            const float u = P.one_m_lmax * (w[j].cv * P.invN) + ljl * ((w[j].jp + w[j].jv) * P.invN);
+            if (j == 0) {
+                us = u;
+                tx = w[j].tx;
+                tn = w[j].tn;
+                va = w[j].va;
+            } else if (vl[j]) {
+                us += u;
+                tx = fmaxf(tx, w[j].tx);
+                tn = fminf(tn, w[j].tn);
+                va = fmaxf(va, w[j].va);
             }
-            sg[t * 4 + (n == 0 ? 0 : 2)] = a;
-            sg[t * 4 + (n == 0 ? 1 : 3)] = bb;
+        }
+        IRM_STAMP(6);
+        ered_store_wpl<WPL>(vl, cvs, us, tx, tn, va, ext, n0, NWL, red, wave);
+#pragma unroll
+        for (int j = 0; j < WPL; ++j) {
+            const int n = nn[j];
+            if (vl[j] && (n == 0 || n == N - 1)) {  // trajectory.py:183-204 rows 0 and N−1
+                float a = 0.f, bb = 0.f;
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    const float e = q2[j][d] - (n == 0 ? s[d] : g[d]);
+                    a += e * e;
+                    bb += v2[j][d] * v2[j][d];
+                }
+                sg[t * 4 + (n == 0 ? 0 : 2)] = a;
+                sg[t * 4 + (n == 0 ? 1 : 3)] = bb;
+            }
         }
     };
     struct Fin {
@@ -1452,12 +1554,12 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
         int idx;
     };
     auto finalize = [&]() {
-        const float* r0 = red + (t * WPT) * 8;
+        const float* r0 = red + (t * WPTL) * 8;
         float cmax = r0[0];
         int cidx = __float_as_int(r0[1]);
         float usum = r0[2], tx = r0[3], tn = r0[4], va = r0[5];
-        for (int ww = 1; ww < WPT; ++ww) {
-            const float* rw = red + (t * WPT + ww) * 8;
+        for (int ww = 1; ww < WPTL; ++ww) {
+            const float* rw = red + (t * WPTL + ww) * 8;
             amax_step(cmax, cidx, rw[0], __float_as_int(rw[1]));
             usum += rw[2];
             tx = fmaxf(tx, rw[3]);
@@ -1479,23 +1581,27 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
         return f;
     };
     // gradient inputs at (q2, v2), mixed by JᵀJ, into X; returns "b' non-zero away from the endpoints"
-    auto grad_inputs = [&](const WP<D>& w, const float (&q2)[D], const float (&v2)[D], int cidx) {
+    auto grad_inputs = [&](const WP<D> (&w)[WPL], const float (&q2)[WPL][D], const float (&v2)[WPL][D], int cidx) {
         bool bfar = false;
-        if (valid) {
-            float a[D], bb[D];
-            grad_waypoint<D>(P, w, q2, v2, n, cidx, lsg, ljl, s, g, a, bb);
-            const bool endrow = (n == 0 || n == N - 1);
 #pragma unroll
-            for (int k = 0; k < D; ++k) {
-                float ma = 0.f, mb = 0.f;
+        for (int j = 0; j < WPL; ++j) {
+            const int n = nn[j];
+            if (vl[j]) {
+                float a[D], bb[D];
+                grad_waypoint<D>(P, w[j], q2[j], v2[j], n, cidx, lsg, ljl, s, g, a, bb);
+                const bool endrow = (n == 0 || n == N - 1);
 #pragma unroll
-                for (int d = 0; d < D; ++d) {
-                    ma += a[d] * P.JtJ[d * D + k];
-                    mb += bb[d] * P.JtJ[d * D + k];
+                for (int k = 0; k < D; ++k) {
+                    float ma = 0.f, mb = 0.f;
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        ma += a[d] * P.JtJ[d * D + k];
+                        mb += bb[d] * P.JtJ[d * D + k];
+                    }
+                    X[(t * D + k) * ldx + n] = ma;
+                    X[(t * D + k) * ldx + NK + n] = mb;
+                    bfar |= (bb[k] != 0.f) & !endrow;  // branch-free
                 }
-                X[(t * D + k) * ldx + n] = ma;
-                X[(t * D + k) * ldx + NK + n] = mb;
-                bfar |= (bb[k] != 0.f) & !endrow;  // branch-free
             }
         }
         return __ballot(bfar) != 0ull;
@@ -1559,7 +1665,7 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
     float loss;
     bool done = !tvalid;
     {
-        WP<D> w;
+        WP<D> w[WPL];
         evaluate(q, v, false, w);
         __syncthreads();
         const Fin f = finalize();
@@ -1581,16 +1687,17 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
         const bool dense = (fl >> 31) != 0u;
         if (tid == 0) fw[par ^ 1] = 0u;
         // this lane's gradient-input rows (α recovery) and the endpoint velocity rows
-        float e0[D], e1[D], xa[D], xb[D];
-        {
-            const int nr = valid ? n : 0;
+        float e0[D], e1[D], xa[WPL][D], xb[WPL][D];
 #pragma unroll
-            for (int k = 0; k < D; ++k) {
-                const float* xc = X + (t * D + k) * ldx;
-                xa[k] = xc[nr];
-                xb[k] = xc[NK + nr];
-                e0[k] = xc[NK];
-                e1[k] = xc[NK + N - 1];
+        for (int k = 0; k < D; ++k) {
+            const float* xc = X + (t * D + k) * ldx;
+            e0[k] = xc[NK];
+            e1[k] = xc[NK + N - 1];
+#pragma unroll
+            for (int j = 0; j < WPL; ++j) {
+                const int nr = vl[j] ? nn[j] : 0;
+                xa[j][k] = xc[nr];
+                xb[j][k] = xc[NK + nr];
             }
         }
         IRM_STAMP(0);
@@ -1634,20 +1741,23 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
         IRM_STAMP(3);
         __syncthreads();
         IRM_STAMP(4);
-        float q2[D], v2[D];
-        WP<D> w;
+        float q2[WPL][D], v2[WPL][D];
+        WP<D> w[WPL];
         if (!done) {  // wave-uniform
 #pragma unroll
-            for (int k = 0; k < D; ++k) {
-                float ut = dP[(t * D + k) * ldx + n], uv = dP[(t * D + k) * ldx + NK + n];
-                if (!dense) {
-                    ut = fmaf(h0T, e0[k], fmaf(h1T, e1[k], ut));
-                    uv = fmaf(h0V, e0[k], fmaf(h1V, e1[k], uv));
+            for (int j = 0; j < WPL; ++j) {
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    float ut = dP[(t * D + k) * ldx + nn[j]], uv = dP[(t * D + k) * ldx + NK + nn[j]];
+                    if (!dense) {
+                        ut = fmaf(h0T[j], e0[k], fmaf(h1T[j], e1[k], ut));
+                        uv = fmaf(h0V[j], e0[k], fmaf(h1V[j], e1[k], uv));
+                    }
+                    dra[j][k] = vl[j] ? xa[j][k] : 0.f;
+                    drb[j][k] = vl[j] ? xb[j][k] : 0.f;
+                    q2[j][k] = cfac * q[j][k] - step * ut;
+                    v2[j][k] = cfac * v[j][k] - step * uv;
                 }
-                dra[k] = valid ? xa[k] : 0.f;
-                drb[k] = valid ? xb[k] : 0.f;
-                q2[k] = cfac * q[k] - step * ut;
-                v2[k] = cfac * v[k] - step * uv;
             }
             IRM_STAMP(5);
             evaluate(q2, v2, false, w);
@@ -1665,11 +1775,14 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
                 done = true;  // minimized: the step is discarded (optimizer_GD.py:304-306)
             } else {
 #pragma unroll
-                for (int k = 0; k < D; ++k) {
-                    q[k] = q2[k];
-                    v[k] = v2[k];
-                    aca[k] = cfac * aca[k] + step * dra[k];  // α recovery: Σ steps·[a'; b']
-                    acb[k] = cfac * acb[k] + step * drb[k];
+                for (int j = 0; j < WPL; ++j) {
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        q[j][k] = q2[j][k];
+                        v[j][k] = v2[j][k];
+                        aca[j][k] = cfac * aca[j][k] + step * dra[j][k];  // α recovery: Σ steps·[a'; b']
+                        acb[j][k] = cfac * acb[j][k] + step * drb[j][k];
+                    }
                 }
                 cprod *= cfac;
                 loss = f.nl;
@@ -1690,11 +1803,14 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
     // α = cprod·α0 − V_R·(Fᵀ·acc)·J⁻¹ in fp32 (k_optimize's PH_RESYNC), T = eval_exact(α),
     // constraintsFulfilled(α) (trajectory.py:129-137, robot.py:90-113).
     st.final_loss = loss;
-    if (valid) {
 #pragma unroll
-        for (int k = 0; k < D; ++k) {
-            X[(t * D + k) * ldx + n] = aca[k];
-            X[(t * D + k) * ldx + NK + n] = acb[k];
+    for (int j = 0; j < WPL; ++j) {
+        if (vl[j]) {
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                X[(t * D + k) * ldx + nn[j]] = aca[j][k];
+                X[(t * D + k) * ldx + NK + nn[j]] = acb[j][k];
+            }
         }
     }
     __syncthreads();
@@ -1704,34 +1820,47 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
 #pragma unroll
         for (int d = 0; d < D; ++d) {
             float y = 0.f;
-            for (int sp = 0; sp < nsplit; ++sp) y += Ypart[(sp * 16 + t * D + d) * ldy + n];
-            Ymix[n * kLd + t * D + d] = y;
+            for (int sp = 0; sp < nsplit; ++sp) y += Ypart[(sp * 16 + t * D + d) * ldy + li];
+            Ymix[li * kLd + t * D + d] = y;
         }
     }
     __syncthreads();
-    if (valid) {
-        float z[D];
 #pragma unroll
-        for (int l = 0; l < D; ++l) z[l] = 0.f;
-        const float* vr = P.Vr + (size_t)n * RP;
-        for (int r = 0; r < RP; ++r) {
-            const float vv = vr[r];
+    for (int j = 0; j < WPL; ++j) {
+        if (vl[j]) {
+            const int n = nn[j];
+            float z[D];
 #pragma unroll
-            for (int l = 0; l < D; ++l) z[l] += vv * Ymix[r * kLd + t * D + l];
+            for (int l = 0; l < D; ++l) z[l] = 0.f;
+            const float* vr = P.Vr + (size_t)n * RP;
+            for (int r = 0; r < RP; ++r) {
+                const float vv = vr[r];
+#pragma unroll
+                for (int l = 0; l < D; ++l) z[l] += vv * Ymix[r * kLd + t * D + l];
+            }
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                float acc = 0.f;
+#pragma unroll
+                for (int l = 0; l < D; ++l) acc += z[l] * P.Jinv[l * D + k];
+                ab[j][k] = cprod * ab[j][k] - acc;
+            }
         }
+    }
+    __syncthreads();  // every lane has read Ymix before X is rewritten below (Ymix is apart; X rows too)
 #pragma unroll
-        for (int k = 0; k < D; ++k) {
-            float acc = 0.f;
+    for (int j = 0; j < WPL; ++j) {
+        if (vl[j]) {
 #pragma unroll
-            for (int l = 0; l < D; ++l) acc += z[l] * P.Jinv[l * D + k];
-            ab[k] = cprod * ab[k] - acc;
-            X[n * kLd + t * D + k] = ab[k];
+            for (int k = 0; k < D; ++k) X[nn[j] * kLd + t * D + k] = ab[j][k];
         }
     }
     __syncthreads();
-    if (valid) eval_exact<D>(P, X + t * D, n, q, v);
+#pragma unroll
+    for (int j = 0; j < WPL; ++j)
+        if (vl[j]) eval_exact<D>(P, X + t * D, nn[j], q[j], v[j]);
     {
-        WP<D> w;
+        WP<D> w[WPL];
         evaluate(q, v, true, w);
     }
     __syncthreads();
@@ -1741,14 +1870,17 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
                         sqrtf(f.b1) < P.eps_v && f.tx <= P.pmax && f.tn >= P.pmin && f.va <= P.vmax;
         st.outer_iterations = 1;
         st.constraints_ok = ok ? 1 : 0;
-        if (valid) {
 #pragma unroll
-            for (int k = 0; k < D; ++k) {
-                if (P.traj_out) P.traj_out[(b * N + n) * D + k] = q[k];
-                if (P.alpha_out) P.alpha_out[(b * N + n) * D + k] = ab[k];
+        for (int j = 0; j < WPL; ++j) {
+            if (vl[j]) {
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    if (P.traj_out) P.traj_out[(b * N + nn[j]) * D + k] = q[j][k];
+                    if (P.alpha_out) P.alpha_out[(b * N + nn[j]) * D + k] = ab[j][k];
+                }
             }
         }
-        if (P.stats && n == 0) P.stats[b] = st;
+        if (P.stats && li == 0) P.stats[b] = st;
     }
     if (tid == 0) prof.flush(P.prof);
 }
@@ -1900,7 +2032,18 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s) {
             // (operators register-resident: one stage-1 unit per wave, enough waves for the units)
             if (p.lean_ok && p.optimizer == IRM_OPT_GD && p.max_outer == 1 && !p.record_series &&
                 (p.RP / 16) * p.nsplit <= p.BT / 64 && p.NK / 16 <= 4 * p.nsplit)
-                return launch_lds(k_gd_single<Sh, TT>, grid, p.BT, lean_lds(p), s, p);
+                return launch_lds(k_gd_single<Sh, TT, 1>, grid, p.BT, lean_lds(p), s, p);
+        }
+        if constexpr (!Sh::kVariants && TT == 1024) {
+            if constexpr (Sh::kNW == 256) {
+                // N = 256 with more than two trajectories per workgroup: two waypoints per lane
+                KParams q = p;
+                q.BT = p.BT / 2;
+                q.NW = p.NW / 2;
+                if (q.lean_ok && q.optimizer == IRM_OPT_GD && q.max_outer == 1 && !q.record_series &&
+                    (q.RP / 16) * q.nsplit <= q.BT / 64 && q.NK / 16 <= 4 * q.nsplit)
+                    return launch_lds(k_gd_single<Sh, 512, 2>, grid, q.BT, lean_lds(q), s, q);
+            }
         }
         auto go = [&](auto bc) {
             constexpr bool BB = decltype(bc)::value;

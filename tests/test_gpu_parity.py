@@ -412,9 +412,11 @@ def test_object_api(g_e2e):
 
 
 @pytest.mark.parametrize("N,mode,D,tb", [(128, "bench", 3, 0), (128, "faithful", 3, 0), (50, "faithful", 3, 0),
-                                        (256, "bench", 3, 2), (256, "faithful", 3, 2), (256, "bench", 7, 2)])
+                                        (256, "bench", 3, 2), (256, "faithful", 3, 2), (256, "bench", 7, 2),
+                                        (256, "bench", 3, 4), (256, "faithful", 3, 4)])
 def test_lean_gd_kernel_matches_general(N, mode, D, tb):
-    """k_gd_single (GD single loop, shape-specialised) vs the general k_optimize
+    """k_gd_single (GD single loop, shape-specialised; at N = 256 with four trajectories per
+    workgroup the two-waypoints-per-lane variant) vs the general k_optimize
     (IRM_GENERAL_KERNEL=1) on the same problems.  Same algorithm and state; the lean kernel feeds
     the MFMAs k-permuted operators (frag_index_kp), so the 4-term partial sums inside each MFMA
     group differently.  The fp32 MFMA accumulates exactly like an fmaf chain and for N ≤ 128 the
