@@ -1488,7 +1488,8 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
     stage_alpha<D>(P, tb0, ntb, X, NK);
     if (tid < 2) fw[tid] = 0u;
     __syncthreads();
-    float q[WPL][D], v[WPL][D], ab[WPL][D], dra[WPL][D], drb[WPL][D], aca[WPL][D], acb[WPL][D];
+    // α0 is not kept in registers: the epilogue restages it (stage_alpha is deterministic)
+    float q[WPL][D], v[WPL][D], aca[WPL][D], acb[WPL][D];
     float s[D], g[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) {
@@ -1500,8 +1501,7 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
 #pragma unroll
         for (int k = 0; k < D; ++k) {
             q[j][k] = v[j][k] = 0.f;
-            dra[j][k] = drb[j][k] = aca[j][k] = acb[j][k] = 0.f;
-            ab[j][k] = vl[j] ? X[nn[j] * kLd + t * D + k] : 0.f;
+            aca[j][k] = acb[j][k] = 0.f;
         }
         if (vl[j]) eval_exact<D>(P, X + t * D, nn[j], q[j], v[j]);  // T0 = (K·α0)·J, V0 = (dK·α0)·J
     }
@@ -1753,8 +1753,6 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
                         ut = fmaf(h0T[j], e0[k], fmaf(h1T[j], e1[k], ut));
                         uv = fmaf(h0V[j], e0[k], fmaf(h1V[j], e1[k], uv));
                     }
-                    dra[j][k] = vl[j] ? xa[j][k] : 0.f;
-                    drb[j][k] = vl[j] ? xb[j][k] : 0.f;
                     q2[j][k] = cfac * q[j][k] - step * ut;
                     v2[j][k] = cfac * v[j][k] - step * uv;
                 }
@@ -1780,8 +1778,9 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
                     for (int k = 0; k < D; ++k) {
                         q[j][k] = q2[j][k];
                         v[j][k] = v2[j][k];
-                        aca[j][k] = cfac * aca[j][k] + step * dra[j][k];  // α recovery: Σ steps·[a'; b']
-                        acb[j][k] = cfac * acb[j][k] + step * drb[j][k];
+                        const float ra = vl[j] ? xa[j][k] : 0.f, rb = vl[j] ? xb[j][k] : 0.f;
+                        aca[j][k] = cfac * aca[j][k] + step * ra;  // α recovery: Σ steps·[a'; b']
+                        acb[j][k] = cfac * acb[j][k] + step * rb;
                     }
                 }
                 cprod *= cfac;
@@ -1803,6 +1802,11 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
     // α = cprod·α0 − V_R·(Fᵀ·acc)·J⁻¹ in fp32 (k_optimize's PH_RESYNC), T = eval_exact(α),
     // constraintsFulfilled(α) (trajectory.py:129-137, robot.py:90-113).
     st.final_loss = loss;
+    float ab[WPL][D];
+#pragma unroll
+    for (int j = 0; j < WPL; ++j)
+#pragma unroll
+        for (int k = 0; k < D; ++k) ab[j][k] = 0.f;
 #pragma unroll
     for (int j = 0; j < WPL; ++j) {
         if (vl[j]) {
@@ -1815,6 +1819,7 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
     }
     __syncthreads();
     stage1(true);
+    stage_alpha<D>(P, tb0, ntb, dP, NK);  // α0 again, row-major into the (free) Δ buffer
     __syncthreads();
     if (yrow) {
 #pragma unroll
@@ -1843,11 +1848,11 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
                 float acc = 0.f;
 #pragma unroll
                 for (int l = 0; l < D; ++l) acc += z[l] * P.Jinv[l * D + k];
-                ab[j][k] = cprod * ab[j][k] - acc;
+                ab[j][k] = cprod * dP[n * kLd + t * D + k] - acc;
             }
         }
     }
-    __syncthreads();  // every lane has read Ymix before X is rewritten below (Ymix is apart; X rows too)
+    __syncthreads();  // X is rewritten below
 #pragma unroll
     for (int j = 0; j < WPL; ++j) {
         if (vl[j]) {
@@ -2035,7 +2040,7 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s) {
                 return launch_lds(k_gd_single<Sh, TT, 1>, grid, p.BT, lean_lds(p), s, p);
         }
         if constexpr (!Sh::kVariants && TT == 1024) {
-            if constexpr (Sh::kNW == 256) {
+            if constexpr (Sh::kNW == 256 && Sh::D * 3 <= kCols) {  // ≥ 3 trajectories fit the MFMA columns
                 // N = 256 with more than two trajectories per workgroup: two waypoints per lane
                 KParams q = p;
                 q.BT = p.BT / 2;
