@@ -644,6 +644,8 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
     {
         const char* g = getenv("IRM_GENERAL_KERNEL");  // diagnostics: force the general optimiser
         kp.lean_ok = (g && g[0] == '1') ? 0 : 1;
+        const char* w = getenv("IRM_LEAN_WPL");
+        kp.lean_wpl = w ? atoi(w) : 0;
     }
     c->max_series = p->max_series > 0 ? p->max_series : 1 + p->max_outer_iteration * p->max_inner_iteration;
     kp.max_series = c->max_series;

@@ -1399,14 +1399,14 @@ __device__ __forceinline__ void ered_store_wpl(const bool (&live)[WPL], const fl
 }
 
 template <class S, int MAXT, int WPL>
-__global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams P) {
+__global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_single(KParams P) {
     constexpr int D = S::D;
     constexpr int S1Q = kS1Q(MAXT);
     // stage-2 tiles per wave: all of this shape's tiles over the workgroup's waves (N = 256: 4)
     constexpr int S2T = (S::MP / 16 + MAXT / 64 - 1) / (MAXT / 64) > kS2T(MAXT)
                             ? (S::MP / 16 + MAXT / 64 - 1) / (MAXT / 64)
                             : kS2T(MAXT);
-    constexpr bool RV = MAXT > 256;  // velocity half of stage 1 register-resident too
+    constexpr bool RV = MAXT > 256 || WPL > 1;  // velocity half of stage 1 register-resident too
     constexpr int NWL = S::NW / WPL;  // lanes per trajectory
     constexpr int WPTL = NWL / 64;    // waves per trajectory
     static_assert(NWL % 64 == 0, "whole waves per trajectory");
@@ -1761,7 +1761,12 @@ __global__ __launch_bounds__(MAXT, MAXT <= 256 ? 2 : 1) void k_gd_single(KParams
             evaluate(q2, v2, false, w);
         }
         IRM_STAMP(7);
-        __syncthreads();
+        if constexpr (WPTL > 1) {
+            __syncthreads();  // the trajectory's wave partials come from several waves
+        } else {              // one wave per trajectory: its own LDS writes, in order
+            __builtin_amdgcn_wave_barrier();
+            asm volatile("" ::: "memory");
+        }
         IRM_STAMP(8);
         if (!done) {
             const Fin f = finalize();
@@ -2033,6 +2038,17 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s) {
     if (grid <= 0) return hipSuccess;
     return dispatch_t(p.BT, [&](auto tc) {
         constexpr int TT = decltype(tc)::value;
+        if constexpr (!Sh::kVariants && TT == 512) {
+            if constexpr (Sh::kNW == 128) {
+                // diagnostic (IRM_LEAN_WPL=2): one wave per trajectory, two waypoints per lane
+                KParams q = p;
+                q.BT = p.BT / 2;
+                q.NW = p.NW / 2;
+                if (p.lean_wpl == 2 && q.lean_ok && q.optimizer == IRM_OPT_GD && q.max_outer == 1 &&
+                    !q.record_series && (q.RP / 16) * q.nsplit <= q.BT / 64 && q.NK / 16 <= 8 * q.nsplit)
+                    return launch_lds(k_gd_single<Sh, 256, 2>, grid, q.BT, lean_lds(q), s, q);
+            }
+        }
         if constexpr (!Sh::kVariants && TT <= 512) {  // GD single loop: the lean kernel
             // (operators register-resident: one stage-1 unit per wave, enough waves for the units)
             if (p.lean_ok && p.optimizer == IRM_OPT_GD && p.max_outer == 1 && !p.record_series &&
