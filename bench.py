@@ -35,6 +35,8 @@ CONFIGS = {
     "c5": ("7-DoF arm, batch of 512 per GPU (4096 on 8), N=256, 11 obstacles, GD (BASELINE configs[4])",
            512, 256, 7, 11, "gd"),
     "c2": ("single trajectory, N=128, 10 obstacles, BLS (BASELINE configs[1])", 1, 128, 3, 10, "bls"),
+    # north_star's stated target shape: a batch of 7-DoF, 128-waypoint trajectories
+    "c7": ("north_star target: 7-DoF arm, batch of 1024 per GPU, N=128, 11 obstacles, GD", 1024, 128, 7, 11, "gd"),
     # diagnostic shapes (not BASELINE configurations): C3's batch at other trajectory lengths
     "c3n64": ("diagnostic: C3 batch at N=64", 1024, 64, 3, 11, "gd"),
     "c3n256": ("diagnostic: C3 batch at N=256", 1024, 256, 3, 11, "gd"),
@@ -65,7 +67,7 @@ def make_problem(cfg, world, rank):
         if O > len(OBSTACLES):  # diagnostic: shifted copies of the reference set
             reps = -(-O // len(OBSTACLES))
             obstacles = np.concatenate([OBSTACLES + 0.1 * i for i in range(reps)])[:O].astype(np.float32)
-        rs = np.random.default_rng(4 if cfg == "c5" else 1)
+        rs = np.random.default_rng({"c5": 4, "c7": 7}.get(cfg, 1))
     start = rs.uniform(-0.5, 0.5, (Btot, D)).astype(np.float32)
     goal = rs.uniform(0.2, 1.6, (Btot, D)).astype(np.float32)
     if cfg == "c2":

@@ -23,7 +23,7 @@ HEADERS = [os.path.join(CSRC, h) for h in ("irm_kernels.hpp", "irm_kernels_impl.
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-unused-function"]
-FIX_SHAPES = [(3, 50), (3, 64), (3, 128), (3, 256), (7, 256)]  # IRM_FIX_SHAPES in irm_kernels_impl.hpp
+FIX_SHAPES = [(3, 50), (3, 64), (3, 128), (3, 256), (7, 128), (7, 256)]  # IRM_FIX_SHAPES in irm_kernels_impl.hpp
 MAX_D = 8
 
 VARIANTS = {

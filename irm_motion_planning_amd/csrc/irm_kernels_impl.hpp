@@ -2092,7 +2092,7 @@ hipError_t launch_forward_dim(const KParams& p, int mode, hipStream_t s) {
 }
 
 // Instantiated in irm_opt_inst.hip (IRM_INST_* macros); irm_kernels.hip only dispatches.
-#define IRM_FIX_SHAPES(X) X(3, 50) X(3, 64) X(3, 128) X(3, 256) X(7, 256)
+#define IRM_FIX_SHAPES(X) X(3, 50) X(3, 64) X(3, 128) X(3, 256) X(7, 128) X(7, 256)
 #define IRM_EXTERN_FIX(D_, N_) extern template hipError_t launch_optimize_shape<FixShape<D_, N_, 32>>(const KParams&, hipStream_t);
 #define IRM_EXTERN_DYN(D_)                                                                          \
     extern template hipError_t launch_optimize_shape<DynShape<D_>>(const KParams&, hipStream_t); \

@@ -293,7 +293,7 @@ def _bench_vs_ref(cfg, B, n_check, iters=200, lmax=None, slack=1e-3):
     return c, alpha, traj, st
 
 
-@pytest.mark.parametrize("cfg,B", [("c3", 256), ("c4", 32), ("c5", 16)])
+@pytest.mark.parametrize("cfg,B", [("c3", 256), ("c4", 32), ("c5", 16), ("c7", 32)])
 def test_bench_smooth_objective_tracks_exact_iteration(cfg, B):
     """λmax = 0 (mean obstacle cost only): 200 steps within 2e-3 (+ sensitivity) of exact."""
     _bench_vs_ref(cfg, B, 4, lmax=0.0)
@@ -317,6 +317,11 @@ def test_bench_c4_random_obstacles():
 
 def test_bench_c5_seven_dof():
     _bench_vs_ref("c5", 32, 3, slack=ARGMAX_SLACK)
+
+
+def test_bench_c7_seven_dof_n128():
+    """north_star's target shape (7-DoF, 128 waypoints; FixShape<7, 128>, lean kernel)."""
+    _bench_vs_ref("c7", 64, 4, slack=ARGMAX_SLACK)
 
 
 def test_per_problem_obstacles_and_edge_counts():
@@ -413,7 +418,8 @@ def test_object_api(g_e2e):
 
 @pytest.mark.parametrize("N,mode,D,tb", [(128, "bench", 3, 0), (128, "faithful", 3, 0), (50, "faithful", 3, 0),
                                         (256, "bench", 3, 2), (256, "faithful", 3, 2), (256, "bench", 7, 2),
-                                        (256, "bench", 3, 4), (256, "faithful", 3, 4)])
+                                        (256, "bench", 3, 4), (256, "faithful", 3, 4),
+                                        (128, "bench", 7, 0), (128, "faithful", 7, 0)])
 def test_lean_gd_kernel_matches_general(N, mode, D, tb):
     """k_gd_single (GD single loop, shape-specialised; at N = 256 with four trajectories per
     workgroup the two-waypoints-per-lane variant) vs the general k_optimize
