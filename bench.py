@@ -109,15 +109,18 @@ def flops_per_iteration(N, D, O, R):
 
 
 def optimiser_kernel(a, info, N, D, opt, B):
-    """Which optimiser kernel the launch uses (mirrors launch_optimize_shape's dispatch)."""
+    """Which optimiser kernel the launch uses (mirrors choose_shape / launch_optimize_shape)."""
     tb = a.tb or min(info["traj_per_block"], -(-B // info["num_cus"]))
     nw = -(-N // 64) * 64
     nk = -(-N // 16) * 16
     nsplit = (nk // 16 + 3) // 4
-    waves = tb * nw // 64
-    wpl = 2 if (nw == 256 and 512 < tb * nw <= 1024) else 1  # N = 256, > 2 trajectories: 2 waypoints/lane
-    lean = (opt == "gd" and not a.faithful and (D, N) in ((3, 50), (3, 64), (3, 128), (3, 256), (7, 256))
-            and info["operator_rank"] == 32 and tb * nw // wpl <= 512 and 2 * nsplit <= waves // wpl)
+    bt = tb * nw
+    if 2 * -(-B // tb) <= info["num_cus"] and bt < 512:
+        bt = 512  # small batch: workgroup padded with trajectory-less waves (IRM_PAD_WAVES)
+    waves = bt // 64
+    wpl = 2 if (nw == 256 and 512 < bt <= 1024) else 1  # N = 256, > 2 trajectories: 2 waypoints/lane
+    lean = (opt == "gd" and not a.faithful and (D, N) in ((3, 50), (3, 64), (3, 128), (3, 256), (7, 128), (7, 256))
+            and info["operator_rank"] == 32 and bt // wpl <= 512 and 2 * nsplit <= waves // wpl)
     return (f"irm::k_gd_single (GD single loop, {wpl} waypoint(s) per lane; fp32 MFMA 16x16x4 + VALU)" if lean
             else "irm::k_optimize (fp32 MFMA 16x16x4 + VALU)")
 

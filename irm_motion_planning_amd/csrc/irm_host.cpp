@@ -219,9 +219,17 @@ int choose_shape(const irm_ctx* c, int B, bool optimizer, KParams& kp, int* lds_
     else if (optimizer) tb = std::min(tbmax, std::max(1, (B + c->num_cus - 1) / std::max(1, c->num_cus)));
     tb = std::max(1, std::min(tb, std::max(1, B)));
     const size_t lds_cap = 160 * 1024;
+    // Under-filled GPU (fewer workgroups than half the CUs: small batches, C2's single
+    // trajectory): pad the optimiser's workgroup with waves that take no trajectory
+    // (tvalid = false in the kernels) up to 512 threads.  They share the MFMA stages (stage-2
+    // tiles and stage-1 units are distributed over all waves), which shortens every round's
+    // latency chain; the per-tile arithmetic is unchanged, so results are bit-identical.
+    const char* pw = getenv("IRM_PAD_WAVES");
+    const bool pad_ok = optimizer && !(pw && pw[0] == '0');
     for (; tb >= 1; --tb) {
         kp.TB = tb;
         kp.BT = tb * kp.NW;
+        if (pad_ok && 2 * ((B + tb - 1) / tb) <= c->num_cus && kp.BT < 512) kp.BT = 512;
         kp.nsplit = irm::stage1_splits(kp.NK);
         if (optimizer) {
             kp.regops = irm::regops_fit(kp) ? 1 : 0;
@@ -460,9 +468,15 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
     }
     // F rows m < N (K part) → row m, m = N + j (dK part) → row NK + j
     auto frow = [&](int m) { return m < N ? m : NK + (m - N); };
-    A.assign((size_t)RP * MP, 0.0);  // Fᵀ (RP × MP): stage 1 contracts y = Fᵀ·[a; b]
-    for (int m = 0; m < 2 * N; ++m)
+    // Fᵀ (RP × MP): stage 1 contracts y = Fᵀ·[a; b].  The endpoint velocity rows (m = N, 2N−1)
+    // are left out: the optimiser adds b'[0], b'[N−1] through their own operator columns (Hend,
+    // Fbot) in every round, so a round whose stage 1 is dense because of a neighbour adds exact
+    // zeros for them and a problem's arithmetic never depends on its workgroup neighbours.
+    A.assign((size_t)RP * MP, 0.0);
+    for (int m = 0; m < 2 * N; ++m) {
+        if (m == N || m == 2 * N - 1) continue;
         for (int r = 0; r < RP; ++r) A[(size_t)r * MP + frow(m)] = F[(size_t)m * RP + r];
+    }
     fill_frag(frag, RP, MP, A);
     rc |= upload(&c->d_F1, frag);
     fill_frag(frag, RP, MP, A, true);

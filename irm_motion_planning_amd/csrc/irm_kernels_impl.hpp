@@ -927,7 +927,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                 if (yrow) {
                     float y[D];
 #pragma unroll
-                    for (int d = 0; d < D; ++d) y[d] = dense ? 0.f : fmaf(fb0, e0[d], fb1 * e1[d]);
+                    for (int d = 0; d < D; ++d) y[d] = fmaf(fb0, e0[d], fb1 * e1[d]);
                     for (int sp = 0; sp < nsplit; ++sp) {
 #pragma unroll
                         for (int d = 0; d < D; ++d) y[d] += Ypart[(sp * RP + n) * kLd + t * D + d];
@@ -1015,10 +1015,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                     dra[k] = valid ? xa[k] : 0.f;
                     drb[k] = valid ? xb[k] : 0.f;
                     float ut = dP[n * kLd + t * D + k], uv = dP[(NK + n) * kLd + t * D + k];
-                    if (!dense) {
-                        ut = fmaf(h0T, e0[k], fmaf(h1T, e1[k], ut));
-                        uv = fmaf(h0V, e0[k], fmaf(h1V, e1[k], uv));
-                    }
+                    // endpoint velocity rows: their operator columns in every round (stage 1's
+                    // operator has zero columns there)
+                    ut = fmaf(h0T, e0[k], fmaf(h1T, e1[k], ut));
+                    uv = fmaf(h0V, e0[k], fmaf(h1V, e1[k], uv));
                     dT[k] = ut;
                     dV[k] = uv;
                 }
@@ -1066,7 +1066,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
             if (rs && yrow) {
 #pragma unroll
                 for (int d = 0; d < D; ++d) {
-                    float y = 0.f;
+                    // endpoint velocity rows through F's endpoint rows (stage 1's operator omits them)
+                    float y = fmaf(fb0, X[NK * kLd + t * D + d], fb1 * X[(NK + N - 1) * kLd + t * D + d]);
                     for (int sp = 0; sp < nsplit; ++sp) y += Ypart[(sp * RP + n) * kLd + t * D + d];
                     Ymix[n * kLd + t * D + d] = y;
                 }
@@ -1749,10 +1750,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
 #pragma unroll
                 for (int k = 0; k < D; ++k) {
                     float ut = dP[(t * D + k) * ldx + nn[j]], uv = dP[(t * D + k) * ldx + NK + nn[j]];
-                    if (!dense) {
-                        ut = fmaf(h0T[j], e0[k], fmaf(h1T[j], e1[k], ut));
-                        uv = fmaf(h0V[j], e0[k], fmaf(h1V[j], e1[k], uv));
-                    }
+                    // endpoint velocity rows enter through their operator columns in every round
+                    // (stage 1's operator has zero columns there: a dense round adds exact zeros)
+                    ut = fmaf(h0T[j], e0[k], fmaf(h1T[j], e1[k], ut));
+                    uv = fmaf(h0V[j], e0[k], fmaf(h1V[j], e1[k], uv));
                     q2[j][k] = cfac * q[j][k] - step * ut;
                     v2[j][k] = cfac * v[j][k] - step * uv;
                 }
@@ -1827,9 +1828,12 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
     stage_alpha<D>(P, tb0, ntb, dP, NK);  // α0 again, row-major into the (free) Δ buffer
     __syncthreads();
     if (yrow) {
+        const float fb0 = P.Fbot[li], fb1 = P.Fbot[(size_t)(N - 1) * RP + li];
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            float y = 0.f;
+            // endpoint velocity rows through F's endpoint rows (stage 1's operator omits them)
+            const float* xc = X + (t * D + d) * ldx;
+            float y = fmaf(fb0, xc[NK], fb1 * xc[NK + N - 1]);
             for (int sp = 0; sp < nsplit; ++sp) y += Ypart[(sp * 16 + t * D + d) * ldy + li];
             Ymix[li * kLd + t * D + d] = y;
         }

@@ -324,6 +324,36 @@ def test_bench_c7_seven_dof_n128():
     _bench_vs_ref("c7", 64, 4, slack=ARGMAX_SLACK)
 
 
+@pytest.mark.parametrize("cfg", ["c3", "c4", "c7"])
+def test_result_independent_of_workgroup_neighbours(cfg):
+    """Several trajectories share a workgroup (their MFMA columns) and a round runs the dense
+    stage 1 when any of them has joint-velocity gradient rows away from the endpoints.  The
+    endpoint velocity rows always enter through their operator columns and X holds zeros there
+    (Head::xe), so a dense round adds exact zeros to a trajectory that does not need it: a
+    problem's result is bit-identical whatever its neighbours — permuted batch, other
+    trajectories-per-workgroup, or solved alone (tools/perm_check.py measured 7 % / 78 % of
+    C3 / C4 problems moving by up to 1e-3 / 0.9 under permutation before this)."""
+    import bench
+    from irm_motion_planning_amd.context import Context
+    from irm_motion_planning_amd.params import params_from_args
+    args = bench.make_args(cfg, False, 200)
+    s, g, obs = bench.make_problem(cfg, 1, 0)
+    B = 64
+    s, g = s[:B], g[:B]
+    tb = 4 if s.shape[1] == 3 else 2  # the bench's workgroup (C4: two waypoints per lane)
+    c = Context(params_from_args(args, traj_per_block=tb))
+    _, traj, st = c.optimize(s, g, obs)
+    perm = np.random.default_rng(3).permutation(B)
+    _, traj_p, _ = c.optimize(s[perm], g[perm], obs)
+    np.testing.assert_array_equal(traj_p, traj[perm])
+    if cfg == "c4":  # alone vs neighbours needs the same waypoints-per-lane variant: 2 per workgroup
+        _, traj, _ = Context(params_from_args(args, traj_per_block=2)).optimize(s, g, obs)
+    c1 = Context(params_from_args(args, traj_per_block=1))
+    for b in (0, 17, 63):
+        _, t1, _ = c1.optimize(s[b:b + 1], g[b:b + 1], obs)
+        np.testing.assert_array_equal(t1[0], traj[b])
+
+
 def test_per_problem_obstacles_and_edge_counts():
     """obstacle_stride > 0: each problem its own obstacle set; also O = 0 and O = 64."""
     args = ("--optimizer-name", "gd", "--max-outer-iteration", 1, "--max-inner-iteration", 30)
@@ -423,15 +453,16 @@ def test_object_api(g_e2e):
 def test_lean_gd_kernel_matches_general(N, mode, D, tb):
     """k_gd_single (GD single loop, shape-specialised; at N = 256 with four trajectories per
     workgroup the two-waypoints-per-lane variant) vs the general k_optimize
-    (IRM_GENERAL_KERNEL=1) on the same problems.  Same algorithm and state; the lean kernel feeds
-    the MFMAs k-permuted operators (frag_index_kp), so the 4-term partial sums inside each MFMA
-    group differently.  The fp32 MFMA accumulates exactly like an fmaf chain and for N ≤ 128 the
-    results are bit-equal on MI355X; at N = 256 the general kernel reads its operators from memory
-    in another tiling, and the bound allows the ulp-level differences GD carries along (waypoints
-    within 2e-3, final loss within 2e-4 relative).  In
-    faithful mode a trajectory whose last improvement sits within rounding of
-    loop_loss_reduction may stop one step earlier or later: at most 10 % of the problems, and
-    the others agree as above."""
+    (IRM_GENERAL_KERNEL=1) on the same problems.  Same algorithm and state, but the lean kernel
+    feeds the MFMAs k-permuted operators (frag_index_kp), so the 4-term partial sums inside each
+    MFMA group differently and the two kernels are two fp32 roundings of the same iteration
+    (tools/pad_check.py: never bit-equal once the lean kernel runs).  B = 48 problems occupy
+    48 workgroups at tb = 0, so the launch is padded to 512 threads (IRM_PAD_WAVES), which is
+    what makes the lean kernel eligible at one trajectory per workgroup.  Bound: waypoints
+    within 5e-3 (1e-2 at D = 7; measured ≤ 3.7e-3 / 4.6e-3 at N = 128 after 60 steps; each kernel separately tracks the
+    exact-arithmetic iteration, test_bench_*), final loss within 2e-4 relative.  In faithful mode
+    a trajectory whose last improvement sits within rounding of loop_loss_reduction may stop one
+    step earlier or later: at most 10 % of the problems, and the others agree as above."""
     from irm_motion_planning_amd.context import Context
     argv = ["--optimizer-name", "gd", "--max-outer-iteration", "1", "--n-timesteps", str(N), "--n-joints", str(D)]
     if D != 3:
@@ -456,14 +487,42 @@ def test_lean_gd_kernel_matches_general(N, mode, D, tb):
     assert same.mean() >= 0.9, same.mean()
     for k in ("outer_iterations",):
         np.testing.assert_array_equal(st1[k], st2[k], err_msg=k)
-    np.testing.assert_allclose(t1[same], t2[same], rtol=0, atol=2e-3)
+    np.testing.assert_allclose(t1[same], t2[same], rtol=0, atol=5e-3 if D == 3 else 1e-2)
     # 2e-4: the λmax > 0 band (a near-tie of two waypoints' costs may pick a different argmax for
-    # one step when the summation differs — at N = 256 the general kernel takes its operators from
-    # memory in another tiling, and 1–2 of 48 problems move by ≤ 1e-4)
+    # one step when the rounding differs; 1–2 of 48 problems move by ≤ 1e-4)
     np.testing.assert_allclose(st1["final_loss"][same], st2["final_loss"][same], rtol=2e-4)
     np.testing.assert_array_equal(t1, lean.evaluate(a1))  # traj_out == K·α_out·J exactly
     print(f"N={N} D={D} tb={tb} {mode}: same step counts {same.mean():.2f}, bit-equal {np.mean(np.all(t1 == t2, axis=(1, 2))):.2f}, "
           f"max |dT| {np.abs(t1[same] - t2[same]).max():.2e}")
+
+
+@pytest.mark.parametrize("optimizer,N,B", [("bls", 128, 1), ("bls", 50, 4), ("gd", 128, 8)])
+def test_wave_padding_is_bit_identical(optimizer, N, B):
+    """Small batches (fewer workgroups than half the CUs) run the general optimiser with its
+    workgroup padded to 512 threads (choose_shape, irm_host.cpp): the extra waves take no
+    trajectory and only share the MFMA tiles, whose arithmetic does not depend on which wave
+    computes them.  Results must be bit-identical to the unpadded launch (IRM_PAD_WAVES=0)."""
+    from irm_motion_planning_amd.context import Context
+    argv = ["--optimizer-name", optimizer, "--n-timesteps", str(N)]
+    rng = np.random.default_rng(17)
+    s = rng.uniform(-0.5, 0.5, (B, 3)).astype(np.float32)
+    g = rng.uniform(0.2, 1.6, (B, 3)).astype(np.float32)
+    s[0], g[0] = START, GOAL
+    out = {}
+    for pad in ("1", "0"):
+        os.environ["IRM_PAD_WAVES"] = pad
+        os.environ["IRM_GENERAL_KERNEL"] = "1"
+        try:
+            c = Context(params(*argv))
+        finally:
+            del os.environ["IRM_PAD_WAVES"], os.environ["IRM_GENERAL_KERNEL"]
+        out[pad] = c.optimize(s, g, obstacles())
+    for x, y in zip(out["1"], out["0"]):
+        if isinstance(x, dict):
+            for k in x:
+                np.testing.assert_array_equal(x[k], y[k], err_msg=k)
+        else:
+            np.testing.assert_array_equal(x, y)
 
 
 @pytest.mark.parametrize("N,D,links", [(33, 3, None), (100, 3, None), (96, 4, [1.0, 0.8, 0.6, 0.4]),
