@@ -1399,14 +1399,16 @@ __device__ __forceinline__ void ered_store_wpl(const bool (&live)[WPL], const fl
     }
 }
 
-template <class S, int MAXT, int WPL>
+// FULL: the launch has exactly MAXT threads, so the stage-2 tiles per wave are known exactly
+// (otherwise kS2T(MAXT) bounds them for smaller launches): C7's 256-thread variant then holds 4
+// tiles of operator fragments instead of 8 (32 VGPRs) and does not spill.
+template <class S, int MAXT, int WPL, bool FULL = false>
 __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_single(KParams P) {
     constexpr int D = S::D;
     constexpr int S1Q = kS1Q(MAXT);
     // stage-2 tiles per wave: all of this shape's tiles over the workgroup's waves (N = 256: 4)
-    constexpr int S2T = (S::MP / 16 + MAXT / 64 - 1) / (MAXT / 64) > kS2T(MAXT)
-                            ? (S::MP / 16 + MAXT / 64 - 1) / (MAXT / 64)
-                            : kS2T(MAXT);
+    constexpr int S2X = (S::MP / 16 + MAXT / 64 - 1) / (MAXT / 64);
+    constexpr int S2T = (FULL || S2X > kS2T(MAXT)) ? S2X : kS2T(MAXT);
     constexpr bool RV = MAXT > 256 || WPL > 1;  // velocity half of stage 1 register-resident too
     constexpr int NWL = S::NW / WPL;  // lanes per trajectory
     constexpr int WPTL = NWL / 64;    // waves per trajectory
@@ -1416,7 +1418,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
     const Head H = plan_head(sh.MP, sh.RP, sh.NSPLIT, true);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nwaves = P.BT >> 6;
+    const int nwaves = FULL ? MAXT / 64 : P.BT >> 6;
     const int N = sh.N, TB = P.TB, RP = sh.RP, MP = sh.MP, NK = sh.NK;
     const int t = wave / WPTL;
     const int li = tid - t * NWL;               // this lane within its trajectory
@@ -2057,7 +2059,8 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s) {
             // (operators register-resident: one stage-1 unit per wave, enough waves for the units)
             if (p.lean_ok && p.optimizer == IRM_OPT_GD && p.max_outer == 1 && !p.record_series &&
                 (p.RP / 16) * p.nsplit <= p.BT / 64 && p.NK / 16 <= 4 * p.nsplit)
-                return launch_lds(k_gd_single<Sh, TT, 1>, grid, p.BT, lean_lds(p), s, p);
+                return p.BT == TT ? launch_lds(k_gd_single<Sh, TT, 1, true>, grid, p.BT, lean_lds(p), s, p)
+                                  : launch_lds(k_gd_single<Sh, TT, 1>, grid, p.BT, lean_lds(p), s, p);
         }
         if constexpr (!Sh::kVariants && TT == 1024) {
             if constexpr (Sh::kNW == 256 && Sh::D * 3 <= kCols) {  // ≥ 3 trajectories fit the MFMA columns
