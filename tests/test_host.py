@@ -90,7 +90,7 @@ def test_bls_norms_in_reduced_space(N):
 
 def test_bench_problems_shard_disjointly():
     import bench
-    for cfg in ("c3", "c4", "c5"):
+    for cfg in ("c3", "c4", "c5", "c7"):
         _, B, N, D, O, _ = bench.CONFIGS[cfg]
         s0, g0, o0 = bench.make_problem(cfg, 2, 0)
         s1, g1, o1 = bench.make_problem(cfg, 2, 1)
@@ -109,6 +109,23 @@ def test_bench_flop_model():
     exec_f, ref_f = bench.flops_per_iteration(128, 3, 11, 32)
     assert ref_f == 12 * 128 * 128 * 3 + 10 * 128 * 9 + 22 * 128 * 11 == 632320
     assert 0 < exec_f < ref_f
+
+
+def test_bench_kernel_label_mirrors_dispatch():
+    """bench.py names the optimiser kernel a launch uses (mirrors choose_shape / launch_optimize_shape):
+    the lean GD kernel for the bench-mode BASELINE shapes, the general one for BLS / faithful runs."""
+    import argparse
+
+    import bench
+    info = {"traj_per_block": 5, "num_cus": 256, "operator_rank": 32}
+    for cfg, want in (("c3", "1 waypoint(s)"), ("c4", "2 waypoint(s)"), ("c5", "1 waypoint(s)"),
+                      ("c7", "1 waypoint(s)"), ("c2", "k_optimize")):
+        _, B, N, D, O, opt = bench.CONFIGS[cfg]
+        a = argparse.Namespace(tb=0, faithful=False)
+        i = dict(info, traj_per_block=16 // D)
+        assert want in bench.optimiser_kernel(a, i, N, D, opt, B), cfg
+    a = argparse.Namespace(tb=0, faithful=True)
+    assert "k_optimize" in bench.optimiser_kernel(a, info, 128, 3, "gd", 1024)
 
 
 def test_bench_args_bench_mode():
