@@ -143,6 +143,7 @@ def cpu_baseline(cfg, args, start, goal, obstacles, budget_s=12.0):
     dt = time.perf_counter() - t0
     iters = sum(s["grad_evals"] for s in st)
     return {"value": iters / dt, "unit": "GD iterations/s", "cores": cores, "kind": "port",
+            "value_1thread": st1[0]["grad_evals"] / t1,  # 1-thread and all-cores rates
             "sample": f"{n} of the {len(start)} rank-0 problems, full optimize() each ({iters} iterations, "
                       f"{dt:.2f} s wall on {cores} threads); 1-thread rate {st1[0]['grad_evals'] / t1:.1f} it/s"}
 
