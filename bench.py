@@ -192,6 +192,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--operator-rank", type=int, default=0)
     ap.add_argument("--tb", type=int, default=0, help="trajectories per workgroup (0 = auto)")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="gloo: rehearse the multi-rank path with host-side collectives, ranks may share a GPU")
     a = ap.parse_args()
 
     import torch
@@ -200,10 +202,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gloo = a.dist_backend == "gloo"
+    if gloo:  # rehearsal: ranks may outnumber the GPUs of the box (counting devices does not init HIP)
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    cdev = torch.device("cpu") if gloo else dev  # where the collectives' tensors live
 
     from irm_motion_planning_amd.context import Context, batch_dev
     from irm_motion_planning_amd._abi import IrmStats
@@ -214,7 +223,7 @@ def main():
     start, goal, obstacles = make_problem(a.config, world, rank)
 
     # shared environment: rank 0's obstacles broadcast over RCCL/xGMI
-    obs_t = share_environment(torch.from_numpy(obstacles).to(dev), world)
+    obs_t = share_environment(torch.from_numpy(obstacles).to(cdev), world).to(dev)
     start_t = torch.from_numpy(start).to(dev)
     goal_t = torch.from_numpy(goal).to(dev)
     alpha_t = torch.empty((B, N, D), dtype=torch.float32, device=dev)
@@ -250,7 +259,7 @@ def main():
 
     st = stats_t.cpu().numpy()
     iters_rank = float(st[:, 2].sum())  # grad_evals = executed inner iterations
-    elapsed_max, iters_all = aggregate(elapsed, iters_rank, world, dev)
+    elapsed_max, iters_all = aggregate(elapsed, iters_rank, world, cdev)
     value = iters_all * a.steps / elapsed_max
 
     exec_f, ref_f = flops_per_iteration(N, D, O, info["operator_rank"])
