@@ -618,6 +618,12 @@ struct DynShape {
 };
 constexpr int kS1Q(int maxt) { return maxt <= 256 ? 8 : 4; }   // stage-1 float4 per wave
 constexpr int kS2T(int maxt) { return maxt <= 256 ? 8 : 2; }   // stage-2 tiles per wave (KQ2 ≤ 2)
+// MP of a shape-specialised shape (0 for DynShape, whose MP is a run-time value)
+template <class S>
+constexpr int shape_mp() {
+    if constexpr (S::kNW > 0) return S::MP;
+    else return 0;
+}
 
 // Row layout of the optimiser's [a; b] / [T; V] buffers and of F: the velocity
 // half starts at row NK (= N rounded up to 16), so the position half is whole
@@ -635,18 +641,22 @@ constexpr int kS2T(int maxt) { return maxt <= 256 ? 8 : 2; }   // stage-2 tiles 
 // α is not carried: each lane accumulates the gradient inputs of the accepted
 // steps (acc = c·acc + s·[a'; b']), and α = cprod·α_base − V_R·Fᵀ·acc·J⁻¹ is
 // formed only when an inner loop ends (PH_RESYNC).
-template <class S, int MAXT, bool OPS_LDS, bool REGOPS, bool BLS>
+// FULL (shape-specialised REGOPS launches of exactly MAXT threads): the stage-2 tiles per wave are
+// known exactly, so only those operator fragments occupy VGPRs (as in k_gd_single<…, FULL>).
+template <class S, int MAXT, bool OPS_LDS, bool REGOPS, bool BLS, bool FULL = false>
 // 256-thread workgroups without register-resident operators fit two per CU (≤ 256 VGPRs); the
 // REGOPS variants need more and keep one (they are launched one per CU anyway).
 __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_optimize(KParams P) {
     constexpr int D = S::D;
-    constexpr int S1Q = kS1Q(MAXT), S2T = kS2T(MAXT);
+    static_assert(!FULL || (REGOPS && S::kNW > 0), "FULL: shape-specialised REGOPS variants only");
+    constexpr int S1Q = kS1Q(MAXT);
+    constexpr int S2T = FULL ? (shape_mp<S>() / 16 + MAXT / 64 - 1) / (MAXT / 64) : kS2T(MAXT);
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const S sh(P);
     const Head H = plan_head(sh.MP, sh.RP, sh.NSPLIT, true);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int nwaves = P.BT >> 6;
+    const int nwaves = FULL ? MAXT / 64 : P.BT >> 6;
     const int N = sh.N, NW = sh.NW, TB = P.TB, RP = sh.RP, MP = sh.MP, NK = sh.NK;
     const int WPT = sh.WPT;             // waves per trajectory
     const int t = wave / WPT;           // this lane's trajectory (wave-uniform)
@@ -2076,6 +2086,10 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s) {
         auto go = [&](auto bc) {
             constexpr bool BB = decltype(bc)::value;
             if constexpr (TT <= 512) {
+                if constexpr (!Sh::kVariants) {
+                    if (p.regops && p.BT == TT)
+                        return launch_lds(k_optimize<Sh, TT, true, true, BB, true>, grid, p.BT, lds, s, p);
+                }
                 if (p.regops) return launch_lds(k_optimize<Sh, TT, true, true, BB>, grid, p.BT, lds, s, p);
             }
             return stage ? launch_lds(k_optimize<Sh, TT, true, false, BB>, grid, p.BT, lds, s, p)
