@@ -1489,14 +1489,20 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
                 if (tile < MT2 && i < KQ2) a2[j * 2 + i] = g2[((size_t)tile * KQ2 + i) * 64 + lane];
             }
     }
+    // endpoint operator columns: in VGPRs for one waypoint per lane; with two (C4: 256 VGPRs) they
+    // are read from an LDS copy each round instead, which keeps the variant free of scratch spills
+    constexpr bool kHL = WPL > 1;
+    float* hL = smem + plan_lds(P, false, true).total;  // 2·MP floats (lean_lds)
     float h0T[WPL], h1T[WPL], h0V[WPL], h1V[WPL];
 #pragma unroll
     for (int j = 0; j < WPL; ++j) {
-        h0T[j] = vl[j] ? P.Hend[nn[j]] : 0.f;
-        h1T[j] = vl[j] ? P.Hend[MP + nn[j]] : 0.f;
-        h0V[j] = vl[j] ? P.Hend[NK + nn[j]] : 0.f;
-        h1V[j] = vl[j] ? P.Hend[MP + NK + nn[j]] : 0.f;
+        h0T[j] = (vl[j] && !kHL) ? P.Hend[nn[j]] : 0.f;
+        h1T[j] = (vl[j] && !kHL) ? P.Hend[MP + nn[j]] : 0.f;
+        h0V[j] = (vl[j] && !kHL) ? P.Hend[NK + nn[j]] : 0.f;
+        h1V[j] = (vl[j] && !kHL) ? P.Hend[MP + NK + nn[j]] : 0.f;
     }
+    if constexpr (kHL)
+        for (int e = tid; e < 2 * MP; e += P.BT) hL[e] = P.Hend[e];
     stage_obstacles(P, tb0, ntb, obsL);
     stage_alpha<D>(P, tb0, ntb, X, NK);
     if (tid < 2) fw[tid] = 0u;
@@ -1764,8 +1770,14 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
                     float ut = dP[(t * D + k) * ldx + nn[j]], uv = dP[(t * D + k) * ldx + NK + nn[j]];
                     // endpoint velocity rows enter through their operator columns in every round
                     // (stage 1's operator has zero columns there: a dense round adds exact zeros)
-                    ut = fmaf(h0T[j], e0[k], fmaf(h1T[j], e1[k], ut));
-                    uv = fmaf(h0V[j], e0[k], fmaf(h1V[j], e1[k], uv));
+                    if constexpr (kHL) {
+                        const int r = vl[j] ? nn[j] : 0;
+                        ut = fmaf(hL[r], e0[k], fmaf(hL[MP + r], e1[k], ut));
+                        uv = fmaf(hL[NK + r], e0[k], fmaf(hL[MP + NK + r], e1[k], uv));
+                    } else {
+                        ut = fmaf(h0T[j], e0[k], fmaf(h1T[j], e1[k], ut));
+                        uv = fmaf(h0V[j], e0[k], fmaf(h1V[j], e1[k], uv));
+                    }
                     q2[j][k] = cfac * q[j][k] - step * ut;
                     v2[j][k] = cfac * v[j][k] - step * uv;
                 }
@@ -2040,7 +2052,7 @@ struct type_tag {
 inline size_t lean_lds(const KParams& p) {
     KParams q = p;
     q.regops = 1;
-    return (size_t)plan_lds(q, false, true).total * 4;
+    return (size_t)(plan_lds(q, false, true).total + 2 * p.MP) * 4;  // + the endpoint columns (hL)
 }
 
 // k_optimize<Shape> with the MAXT / operator-placement / optimiser variants (one shape per
