@@ -42,6 +42,7 @@ CONFIGS = {
     "c3n256": ("diagnostic: C3 batch at N=256", 1024, 256, 3, 11, "gd"),
     "c3o0": ("diagnostic: C3 batch without obstacles", 1024, 128, 3, 0, "gd"),
     "c3o44": ("diagnostic: C3 batch, the reference's obstacles ×4 (shifted copies)", 1024, 128, 3, 44, "gd"),
+    "c3b8192": ("diagnostic: C3 problems, 8192 on one GPU (eight workgroups per CU in sequence)", 8192, 128, 3, 11, "gd"),
 }
 
 PEAK_FP32_TFLOPS = 157.3  # MI355X fp32 (vector = matrix), MI355X_MICROARCH.md
@@ -108,9 +109,15 @@ def flops_per_iteration(N, D, O, R):
     return exec_f, ref_f
 
 
+def effective_tb(a, info, B):
+    """Trajectories per workgroup of the launch (choose_shape: info's traj_per_block is the shape's
+    maximum, an explicit --tb is capped by it)."""
+    return min(a.tb, info["traj_per_block"]) if a.tb else min(info["traj_per_block"], -(-B // info["num_cus"]))
+
+
 def optimiser_kernel(a, info, N, D, opt, B):
     """Which optimiser kernel the launch uses (mirrors choose_shape / launch_optimize_shape)."""
-    tb = a.tb or min(info["traj_per_block"], -(-B // info["num_cus"]))
+    tb = effective_tb(a, info, B)
     nw = -(-N // 64) * 64
     nk = -(-N // 16) * 16
     nsplit = (nk // 16 + 3) // 4
@@ -286,7 +293,7 @@ def main():
             "batch_per_gpu": B, "global_batch": B * world, "n_timesteps": N, "n_joints": D, "n_obstacles": O,
             "optimizer": opt, "mode": "faithful" if a.faithful else f"bench ({a.max_inner} fixed GD iterations)",
             "operator_rank": info["operator_rank"],
-            "traj_per_block": a.tb or min(info["traj_per_block"], -(-B // info["num_cus"])),
+            "traj_per_block": effective_tb(a, info, B),
             "parallelism": f"dp{world} (batch sharded, env broadcast over RCCL)",
         },
         "roofline": {

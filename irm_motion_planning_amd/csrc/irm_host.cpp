@@ -213,7 +213,11 @@ int choose_shape(const irm_ctx* c, int B, bool optimizer, KParams& kp, int* lds_
     kp.NW = round_up(c->N, 64);
     // D ≥ 5 needs > 128 VGPRs per lane: keep those workgroups at ≤ 512 threads
     const int maxthreads = (D >= 5) ? 512 : irm::kMaxThreads;
-    const int tbmax = std::max(1, std::min(irm::kCols / D, maxthreads / kp.NW));
+    // Optimiser workgroups of N ≤ 128 stay at ≤ 512 threads: the 1024-thread variants are capped at
+    // 128 VGPRs and spill (C3 with five trajectories per workgroup: 1.47 ms vs 0.79 ms for four), so a
+    // large batch is better served by more 4-trajectory workgroups (bench.py --tb 5 vs default).
+    const int cap = (optimizer && kp.NW <= 128) ? std::min(maxthreads, 512) : maxthreads;
+    const int tbmax = std::max(1, std::min(irm::kCols / D, cap / kp.NW));
     int tb = tbmax;
     if (optimizer && c->p.traj_per_block > 0) tb = std::min(c->p.traj_per_block, tbmax);
     else if (optimizer) tb = std::min(tbmax, std::max(1, (B + c->num_cus - 1) / std::max(1, c->num_cus)));
