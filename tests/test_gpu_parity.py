@@ -354,6 +354,24 @@ def test_result_independent_of_workgroup_neighbours(cfg):
         np.testing.assert_array_equal(t1[0], traj[b])
 
 
+def test_large_batch_matches_small_batch():
+    """4096 C3 problems in one launch (1024 four-trajectory workgroups, four per CU in sequence):
+    every problem bit-identical to the same problem solved in a 1024-batch (workgroup-neighbour
+    independence), so the large-batch rate of bench.py --config c3b8192 computes the same thing."""
+    import bench
+    from irm_motion_planning_amd.context import Context
+    from irm_motion_planning_amd.params import params_from_args
+    args = bench.make_args("c3", False, 40)
+    obs = bench.make_problem("c3", 4, 0)[2]
+    s4 = np.concatenate([bench.make_problem("c3", 4, r)[0] for r in range(4)])
+    g4 = np.concatenate([bench.make_problem("c3", 4, r)[1] for r in range(4)])
+    c = Context(params_from_args(args))
+    _, t_big, st_big = c.optimize(s4, g4, obs)
+    assert t_big.shape[0] == 4096 and np.all(st_big["grad_evals"] == 40)
+    _, t_small, _ = c.optimize(s4[3072:], g4[3072:], obs)
+    np.testing.assert_array_equal(t_big[3072:], t_small)
+
+
 def test_per_problem_obstacles_and_edge_counts():
     """obstacle_stride > 0: each problem its own obstacle set; also O = 0 and O = 64."""
     args = ("--optimizer-name", "gd", "--max-outer-iteration", 1, "--max-inner-iteration", 30)
