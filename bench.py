@@ -168,6 +168,57 @@ def pmc_traffic(cfg):
     return None, None
 
 
+def pmc_flops(cfg):
+    """Issued fp32 flops per optimiser launch from the newest profiles/*_flops.json (rocprofv3 SQ
+    instruction counters of this bench command, tools/pmc_flops.sh), or None."""
+    import glob
+    for path in reversed(sorted(glob.glob(os.path.join(HERE, "profiles", "*_flops.json")))):
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("config", "c3") == cfg and d.get("flops_per_launch"):
+            return float(d["flops_per_launch"]), os.path.relpath(path, HERE)
+    return None, None
+
+
+def config_record(a, args, desc, B, N, D, O, opt, world, info):
+    """The workload as run: shape, mode and every hyper-parameter that departs from main.py's defaults."""
+    from irm_motion_planning_amd import main as irm_main
+    defaults = vars(irm_main.parse_args([]))
+    overrides = {k: v for k, v in vars(args).items() if k in defaults and defaults[k] != v
+                 and k not in ("optimizer_name", "n_timesteps", "n_joints")}
+    return {
+        "workload": f"{a.config}: {desc}",
+        "batch_per_gpu": B, "global_batch": B * world, "n_timesteps": N, "n_joints": D, "n_obstacles": O,
+        "optimizer": opt, "mode": "faithful" if a.faithful else f"bench ({a.max_inner} fixed GD iterations)",
+        "gd_lr_first": float(args.gd_lr[0]),
+        "overrides_vs_reference_defaults": overrides,
+        "operator_rank": None if info is None else info["operator_rank"],
+        "traj_per_block": None if info is None else effective_tb(a, info, B),
+        "parallelism": f"dp{world} (batch sharded, env broadcast over {'gloo' if (a.dist_backend == 'gloo' or a.dry_run) else 'RCCL'})",
+    }
+
+
+def launch_ranks(a):
+    """`bench.py --gpus N` outside torchrun: start N ranks under torch.distributed.run as a CHILD
+    process (nothing in this process has touched HIP) and relay rank 0's JSON line."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1"))
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{") and '"metric"' in ln]
+    for ln in p.stdout.splitlines():
+        if ln not in lines:
+            print(ln, file=sys.stderr)
+    if lines:
+        print(lines[-1], flush=True)
+    return p.returncode if lines or p.returncode else 1
+
+
 def share_environment(obs_t, world):
     """Rank 0's obstacles to every rank (RCCL broadcast over xGMI; gloo in the CPU tests)."""
     if world > 1:
@@ -188,6 +239,36 @@ def aggregate(elapsed, iters_rank, world, device):
     return float(t.item()), float(it.item())
 
 
+def dry_run(a, world, rank):
+    """The multi-rank plumbing of main() without the device: shard, environment broadcast, the
+    max-time / Σ-iterations reduction.  Prints the JSON line with value null."""
+    import torch
+    import torch.distributed as dist
+    desc, B, N, D, O, opt = CONFIGS[a.config]
+    args = make_args(a.config, a.faithful, a.max_inner)
+    start, goal, obstacles = make_problem(a.config, world, rank)
+    obs = share_environment(torch.from_numpy(obstacles + (0.0 if rank == 0 else 1.0)), world)
+    elapsed_max, iters_all = aggregate(1.0 + rank, float(B * a.max_inner), world, "cpu")
+    same = torch.tensor([float(np.array_equal(obs.numpy(), obstacles if rank == 0 else obstacles))])
+    if world > 1:
+        dist.all_reduce(same, op=dist.ReduceOp.MIN)
+    shard = torch.tensor([float(start.sum())], dtype=torch.float64)
+    shards = [torch.zeros_like(shard) for _ in range(world)] if world > 1 else [shard]
+    if world > 1:
+        dist.all_gather(shards, shard)
+    if rank == 0:
+        print(json.dumps({"metric": "GD iterations/sec (batch of trajectories)", "value": None, "dry_run": True,
+                          "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+                          "config": config_record(a, args, desc, B, N, D, O, opt, world, None),
+                          "obstacles_equal_rank0": bool(same.item() == 1.0),
+                          "elapsed_max": elapsed_max, "iterations_all": iters_all,
+                          "shard_checksums": [float(x.item()) for x in shards]}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -201,22 +282,31 @@ def main():
     ap.add_argument("--tb", type=int, default=0, help="trajectories per workgroup (0 = auto)")
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="gloo: rehearse the multi-rank path with host-side collectives, ranks may share a GPU")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / collective plumbing only (no device, no kernel): CPU tests of --gpus N")
     a = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return launch_ranks(a)
 
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        print(f"bench: --gpus {a.gpus} but WORLD_SIZE={world}; reporting the launched world", file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     gloo = a.dist_backend == "gloo"
     if gloo:  # rehearsal: ranks may outnumber the GPUs of the box (counting devices does not init HIP)
         local = local % max(1, torch.cuda.device_count())
     if world > 1:
-        if gloo:
+        if gloo or a.dry_run:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if a.dry_run:
+        return dry_run(a, world, rank)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     cdev = torch.device("cpu") if gloo else dev  # where the collectives' tensors live
@@ -272,9 +362,11 @@ def main():
     exec_f, ref_f = flops_per_iteration(N, D, O, info["operator_rank"])
     launch_flops = exec_f * iters_rank
     achieved = launch_flops / (kernel_ms * 1e-3) / 1e12
-    ref_tflops = ref_f * iters_rank / (kernel_ms * 1e-3) / 1e12
+    dense_tflops = ref_f * iters_rank / (kernel_ms * 1e-3) / 1e12
     bytes_launch = B * (2 * D + 2 * N * D) * 4 + B * 32  # start/goal in; alpha/traj/stats out
-    traffic, traffic_src = pmc_traffic(a.config) if (a.max_inner == 200 and not a.faithful) else (None, None)
+    canonical = a.max_inner == 200 and not a.faithful and a.tb == 0 and a.operator_rank == 0
+    traffic, traffic_src = pmc_traffic(a.config) if canonical else (None, None)
+    counted, counted_src = pmc_flops(a.config) if canonical else (None, None)
     result = {
         "metric": "GD iterations/sec (batch of trajectories)",
         "value": value,
@@ -288,44 +380,41 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (SURVEY.md §8d seeds), reference environment",
-        "config": {
-            "workload": f"{a.config}: {desc}",
-            "batch_per_gpu": B, "global_batch": B * world, "n_timesteps": N, "n_joints": D, "n_obstacles": O,
-            "optimizer": opt, "mode": "faithful" if a.faithful else f"bench ({a.max_inner} fixed GD iterations)",
-            "operator_rank": info["operator_rank"],
-            "traj_per_block": effective_tb(a, info, B),
-            "parallelism": f"dp{world} (batch sharded, env broadcast over RCCL)",
-        },
+        "config": config_record(a, args, desc, B, N, D, O, opt, world, info),
         "roofline": {
-            # achieved = SURVEY.md §8d's algorithmic flops per GD iteration (the reference's dense
-            # α-space formulation, 12N²D + 10ND² + 22NO) × iterations per launch ÷ launch time.
-            # The kernel reaches the same iterate with the rank-R trajectory-space formulation and
-            # executes far fewer flops: executed_* below.
+            # achieved = the flops one launch of THIS algorithm executes (the rank-R trajectory-space
+            # GD iteration, DESIGN.md §5: exec_f per trajectory-iteration × the iterations of the
+            # launch) ÷ the launch's average duration (HIP events on the launch stream).
             "bound": "mfma",
-            "achieved": ref_tflops,
+            "achieved": achieved,
             "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s",
-            "frac": ref_tflops / PEAK_FP32_TFLOPS,
+            "frac": achieved / PEAK_FP32_TFLOPS,
             "traffic": traffic,
             "traffic_source": traffic_src,
             "kernel": optimiser_kernel(a, info, N, D, opt, B),
             "kernel_ms": kernel_ms,
-            "algorithmic_flops_per_iteration": ref_f,
-            "executed_flops_per_iteration": exec_f,
-            "executed_tflops": achieved,
-            "executed_frac": achieved / PEAK_FP32_TFLOPS,
+            "flops_per_iteration": exec_f,
+            "flops_per_launch": launch_flops,
+            # what the hardware issued, from rocprofv3 PMC counters of the same command
+            # (MFMA + f32 VALU lane operations, padding lanes/columns included; tools/pmc_flops.sh)
+            "counted_flops_per_launch": counted,
+            "counted_tflops": None if counted is None else counted / (kernel_ms * 1e-3) / 1e12,
+            "counted_frac": None if counted is None else counted / (kernel_ms * 1e-3) / 1e12 / PEAK_FP32_TFLOPS,
+            "counted_source": counted_src,
+            # SURVEY.md §8d's count of the reference's dense alpha-space formulation, for comparison only:
+            # the same iterations priced at 12N²D + 10ND² + 22NO flops each (this kernel does not execute them)
+            "dense_equivalent_flops_per_iteration": ref_f,
+            "dense_equivalent_tflops": dense_tflops,
+            "dense_equivalent_frac": dense_tflops / PEAK_FP32_TFLOPS,
             "hbm_algorithmic_bytes_per_launch": bytes_launch,
             "hbm_achieved_gbs": bytes_launch / (kernel_ms * 1e-3) / 1e9,
             "hbm_frac": bytes_launch / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
-            "note": "achieved/frac count SURVEY.md 8d's algorithmic flops of the reference's dense alpha-space "
-                    "formulation; the kernel reaches the same iterate with the rank-R trajectory-space operator "
-                    "(executed_flops_per_iteration), so frac > 1 is algorithmic saving and executed_frac is the "
-                    "arithmetic-unit utilisation (DESIGN.md 5)",
         },
         "cpu_baseline": None,
         "iterations_per_step": iters_all,
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and not a.no_cpu_baseline:  # rank 0's host cores, its own shard, every world size
         result["cpu_baseline"] = cpu_baseline(a.config, args, start, goal, obstacles)
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -335,4 +424,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

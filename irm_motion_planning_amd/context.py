@@ -186,6 +186,16 @@ class Context:
         B = s.shape[0]
         obs = _f32(obstacles)
         O = obs.shape[-2] if obs.size else 0
+        if obs.ndim == 3:  # per-problem obstacles B × O × 2: one row of 2·O floats per problem
+            if obs.shape[0] != B or obs.shape[2] != 2:
+                raise ValueError(f"per-problem obstacles must be ({B}, O, 2), got {obs.shape}")
+            if obstacle_stride not in (0, 2 * O):
+                raise ValueError(f"obstacle_stride {obstacle_stride} does not match obstacles {obs.shape}")
+            obstacle_stride = 2 * O
+        elif obs.size and (obs.ndim != 2 or obs.shape[1] != 2):
+            raise ValueError(f"shared obstacles must be (O, 2), got {obs.shape}")
+        elif obstacle_stride:
+            raise ValueError("obstacle_stride needs per-problem obstacles of shape (B, O, 2)")
         a0 = None
         if alpha0 is not None:
             a0 = _f32(alpha0).reshape(B, self.N, self.D)

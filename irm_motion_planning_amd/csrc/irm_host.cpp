@@ -761,6 +761,13 @@ int check_obs(int O) {
     return 0;
 }
 
+// obstacle_stride: 0 = one shared O×2 table, else floats between consecutive problems' tables (≥ 2·O)
+int check_stride(int O, int stride) {
+    if (stride != 0 && (stride < 2 * O || stride < 0))
+        return fail(IRM_EINVAL, "obstacle_stride=%d must be 0 (shared) or >= 2*n_obstacles=%d", stride, 2 * O);
+    return 0;
+}
+
 // Run one forward-family kernel on B host trajectories.
 int run_forward(irm_ctx* c, int mode, const float* alpha, const float* start, const float* goal, const float* obs,
                 int O, int B, float lsg, float ljl, float lmax, int which, float* out0, float* out1, uint8_t* ok) {
@@ -928,7 +935,7 @@ int irm_init_alpha(irm_ctx* c, const float* start, const float* goal, int32_t B,
 int irm_optimize_batch_dev(irm_ctx* c, const irm_batch_dev* a, void* stream) {
     if (!c || !a) return fail(IRM_EINVAL, "irm_optimize_batch_dev: null argument");
     if (a->batch < 0 || !a->start || !a->goal) return fail(IRM_EINVAL, "bad batch arguments");
-    if (check_obs(a->n_obstacles)) return IRM_EINVAL;
+    if (check_obs(a->n_obstacles) || check_stride(a->n_obstacles, a->obstacle_stride)) return IRM_EINVAL;
     if (a->n_obstacles > 0 && !a->obstacles) return fail(IRM_EINVAL, "obstacles pointer missing");
     if (set_device(c)) return IRM_EDEVICE;
     if (a->batch == 0) return IRM_OK;
@@ -966,7 +973,7 @@ int irm_optimize_batch(irm_ctx* c, const float* alpha0, const float* start, cons
                        int32_t O, int32_t obstacle_stride, int32_t B, float* alpha_out, float* traj_out,
                        irm_stats* stats_out, float* series_out) {
     if (!c || !start || !goal) return fail(IRM_EINVAL, "irm_optimize_batch: null argument");
-    if (check_obs(O)) return IRM_EINVAL;
+    if (check_obs(O) || check_stride(O, obstacle_stride)) return IRM_EINVAL;
     if (set_device(c)) return IRM_EDEVICE;
     if (B <= 0) return B == 0 ? IRM_OK : fail(IRM_EINVAL, "negative batch");
     const int N = c->N, D = c->D;

@@ -2,7 +2,7 @@
 // Included by irm_kernels.hip (host-API kernels, launch dispatch) and by the instantiation
 // units irm_opt_inst.hip (one k_optimize shape / k_forward D per object, compiled in parallel).
 //
-// Hot path of simongroeger/irm_motion_planning: optimizer_GD.py:386-445 and
+// Hot path of simongroeger/irm_motion_planning: optimizer_GD.py:173-232 and
 // optimizer_BLS.py:126-213 over trajectory.py:271-297 / robot.py:29-87 /
 // environment.py:32-58.  DESIGN.md describes the formulation:
 //   * the optimiser state is kept in trajectory space, T = K·α·J and
@@ -1186,23 +1186,26 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
             // --------------------------------------------------- decide
             int accept = 0;
             bool snap = false, to_end = false;
-            if (phase == PH_OUTER_START) {  // optimizer_GD.py:422-424 / optimizer_BLS.py:193
+            if (phase == PH_OUTER_START) {  // optimizer_GD.py:209-211 / optimizer_BLS.py:193
                 loss = nl;
                 if (!bls) st.cost_evals++;
                 accept = 2;
                 lr = bls ? cold[C_BLR0] : cold[outer];
                 needs_dir = true;
                 if (!bls) phase = PH_GD_INNER;
-                if (P.max_inner <= 0) to_end = true;
+                // BLS with max_outer_iteration <= 0: the reference's outer while_loop never runs and
+                // optimize() returns α0 (optimizer_BLS.py:184-186, 210-213) — straight to the resync
+                // (α materialised, constraints reported), no outer iteration counted
+                if (P.max_inner <= 0 || (bls && cold_int(C_MAXOUT) <= 0)) to_end = true;
             } else if (phase == PH_BLS_REEVAL) {  // gradient at the unchanged α after a fully rejected search
                 needs_dir = true;
             } else if (phase == PH_RESYNC) {
                 // constraintsFulfilled(α) (trajectory.py:129-137, robot.py:90-113) on the
-                // materialised α; optimizer_GD.py:427-437 / optimizer_BLS.py:201-211
+                // materialised α; optimizer_GD.py:214-224 / optimizer_BLS.py:201-211
                 const float eps_p = cold[C_EPSP], eps_v = cold[C_EPSV];
                 const bool ok = sqrtf(e_a0) < eps_p && sqrtf(e_a1) < eps_p && sqrtf(e_b0) < eps_v &&
                                 sqrtf(e_b1) < eps_v && tx <= cold[C_PMAX] && tn >= cold[C_PMIN] && va <= cold[C_VMAX];
-                st.outer_iterations++;
+                if (!bls || cold_int(C_MAXOUT) > 0) st.outer_iterations++;
                 st.constraints_ok = ok ? 1 : 0;
                 if (ok) {
                     phase = PH_DONE;
@@ -1213,7 +1216,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                     inner = 0;
                     phase = (outer >= cold_int(C_MAXOUT)) ? PH_DONE : PH_OUTER_START;
                 }
-            } else if (phase == PH_GD_INNER) {  // optimizer_GD.py:394-408
+            } else if (phase == PH_GD_INNER) {  // optimizer_GD.py:180-195
                 st.grad_evals++;
                 st.cost_evals++;
                 if (loss - nl < P.llr) {
@@ -1296,7 +1299,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                 cprod *= cfac;
             }
             // extended-vis snapshot after every non-breaking inner iteration
-            // (optimizer_GD.py:366-367, optimizer_BLS.py:106-107)
+            // (optimizer_GD.py:153-154, optimizer_BLS.py:106-107)
             if (rec && snap && st.series_len < cold_int(C_MAXSER)) {
                 if (valid) {
                     float* ser = cold_ptr(0);
@@ -1334,7 +1337,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
 
 // ------------------------------------------- GD single loop, lean optimiser
 // optimizer_GD.py jit_optimize (max_outer_iteration == 1, dualOptimization false;
-// optimizer_GD.py:281-310): g = ∇L(α); α' = (1 − λ_reg·lr)·α − lr·g; accept iff
+// optimizer_GD.py:68-97): g = ∇L(α); α' = (1 − λ_reg·lr)·α − lr·g; accept iff
 // L − L(α') ≥ loop_loss_reduction, else stop keeping α; at most max_inner steps; then
 // α is materialised and constraintsFulfilled decides constraints_ok (k_optimize's
 // PH_RESYNC).  The same arithmetic as k_optimize's GD rounds (bit-identical results for
@@ -1679,7 +1682,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
         *reinterpret_cast<f32x4*>(Ypart + (sp1 * 16 + cl) * ldy + tile1 * 16 + r4) = acc0 + acc1;
     };
 
-    // round 0 (optimizer_GD.py:295: the loss at α0) and the first gradient inputs
+    // round 0 (optimizer_GD.py:93: the loss at α0) and the first gradient inputs
     irm_stats st{};
     float loss;
     bool done = !tvalid;
@@ -1800,7 +1803,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
             st.cost_evals++;
             bool bfar = false;
             if (loss - f.nl < P.llr) {
-                done = true;  // minimized: the step is discarded (optimizer_GD.py:304-306)
+                done = true;  // minimized: the step is discarded (optimizer_GD.py:87-90)
             } else {
 #pragma unroll
                 for (int j = 0; j < WPL; ++j) {

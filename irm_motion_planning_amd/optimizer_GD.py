@@ -1,9 +1,9 @@
 """GradientDescentOptimizer — mirrors optimizer_GD.py (optimizer_GD.py:14-232).
 
 Fixed-step functional gradient descent.  With max_outer_iteration > 1 it is
-the dual loop (jit_dual_optimize, optimizer_GD.py:385-445: per-outer step
+the dual loop (jit_dual_optimize, optimizer_GD.py:173-232: per-outer step
 size gd_lr[outer], λ escalation on violated constraints); with 1 it is the
-single loop (jit_optimize, optimizer_GD.py:281-310).  Both run on device in
+single loop (jit_optimize, optimizer_GD.py:68-97).  Both run on device in
 the persistent kernel k_optimize.
 """
 from ._abi import IrmError
@@ -25,7 +25,7 @@ class GradientDescentOptimizer(_PersistentOptimizer):
     def optimize(self):
         out = super().optimize()
         if not self.jitLoop and not self.dualOptimization and self.last_stats is not None:
-            # plain_optimize prints where the single loop stopped (optimizer_GD.py:324)
+            # plain_optimize prints where the single loop stopped (optimizer_GD.py:111)
             if int(self.last_stats["inner_iterations"]) < self.max_inner_iteration:
                 print("break after", int(self.last_stats["inner_iterations"]), "iteration")
         return out

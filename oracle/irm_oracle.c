@@ -562,8 +562,8 @@ static void snapshot(const orc_ctx* c, const float* alpha, float* series, int32_
     (*len)++;
 }
 
-/* optimizer_GD.py:386-445 (jit_dual_optimize); with max_outer_iteration == 1
-   it reduces to jit_optimize (optimizer_GD.py:281-310). */
+/* optimizer_GD.py:173-232 (jit_dual_optimize); with max_outer_iteration == 1
+   it reduces to jit_optimize (optimizer_GD.py:68-97). */
 static void optimize_gd(const orc_ctx* c, float* alpha, const float* obs, int O, const float* s,
                         const float* g, irm_stats* st, float* series, int32_t max_series) {
     const irm_params* p = &c->p;
@@ -571,12 +571,15 @@ static void optimize_gd(const orc_ctx* c, float* alpha, const float* obs, int O,
     float lsg = p->lambda_sg_constraint, ljl = p->lambda_jl_constraint;
     float grad[IRM_MAX_TIMESTEPS * IRM_MAX_JOINTS], na[IRM_MAX_TIMESTEPS * IRM_MAX_JOINTS];
     int fulfilled = 0, outer = 0;
-    while (outer < p->max_outer_iteration && !fulfilled) {
+    /* dualOptimization = max_outer_iteration > 1 (optimizer_GD.py:18); otherwise the single loop
+       (:54-65) runs once, whatever max_outer_iteration is */
+    const int max_outer = p->max_outer_iteration > 1 ? p->max_outer_iteration : 1;
+    while (outer < max_outer && !fulfilled) {
         float lr = p->gd_lr[outer];
-        float last = orc_cost(c, alpha, obs, O, s, g, lsg, ljl, p->lambda_max_cost); /* :423 */
+        float last = orc_cost(c, alpha, obs, O, s, g, lsg, ljl, p->lambda_max_cost); /* :93 / :210 */
         st->cost_evals++;
         int it = 0, minimized = 0;
-        while (it < p->max_inner_iteration && !minimized) { /* :394-408 */
+        while (it < p->max_inner_iteration && !minimized) { /* :76-91 / :180-195 */
             orc_cost_g(c, alpha, obs, O, s, g, lsg, ljl, p->lambda_max_cost, grad);
             st->grad_evals++;
             float cf = 1.f - p->lambda_reg * lr;
@@ -590,10 +593,10 @@ static void optimize_gd(const orc_ctx* c, float* alpha, const float* obs, int O,
                 memcpy(alpha, na, sizeof(float) * ND);
                 last = nl;
                 st->inner_iterations++;
-                snapshot(c, alpha, series, max_series, &st->series_len); /* optimizer_GD.py:366-367 */
+                snapshot(c, alpha, series, max_series, &st->series_len); /* optimizer_GD.py:153-154 */
             }
         }
-        fulfilled = orc_constraints(c, alpha, s, g, NULL); /* :427 */
+        fulfilled = orc_constraints(c, alpha, s, g, NULL); /* :214 */
         st->outer_iterations++;
         if (!fulfilled) {
             outer++;
@@ -670,6 +673,12 @@ static void optimize_bls(const orc_ctx* c, float* alpha, const float* obs, int O
             lsg *= p->lambda_constraint_increase;
             ljl *= p->lambda_constraint_increase;
         }
+    }
+    /* max_outer_iteration <= 0: the outer while_loop never runs and α0 is returned (:184-186, 210-213);
+       the flag reported is constraintsFulfilled(α0), as main.py:143 would print it */
+    if (p->max_outer_iteration <= 0) {
+        fulfilled = orc_constraints(c, alpha, s, g, NULL);
+        st->final_loss = orc_cost(c, alpha, obs, O, s, g, lsg, ljl, p->lambda_max_cost);
     }
     st->constraints_ok = fulfilled;
 }

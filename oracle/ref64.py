@@ -5,7 +5,7 @@ reference's fp32 arithmetic, this module runs the same algorithm in fp64, so
 that tests can separate (a) fp32 rounding effects of the reference's α-space
 iteration from (b) disagreements in the algorithm.  Citations as in
 irm_oracle.c: trajectory.py:63-297, robot.py:29-113, environment.py:32-58,
-optimizer_GD.py:281-310 / 386-445, optimizer_BLS.py:127-211.
+optimizer_GD.py:68-97 / 386-445, optimizer_BLS.py:127-211.
 """
 import numpy as np
 
@@ -98,7 +98,7 @@ class Ref64:
         return (self.K.T @ a + self.dK.T @ b) @ self.J.T
 
     def gd_single(self, alpha0, obs, s, g, iters, lr=None):
-        """optimizer_GD.py:281-310 in fp64 (single loop, λ at their initial values)."""
+        """optimizer_GD.py:68-97 in fp64 (single loop, λ at their initial values)."""
         p = self.p
         lr = p.gd_lr[0] if lr is None else lr
         lsg, ljl, lmax = p.lambda_sg_constraint, p.lambda_jl_constraint, p.lambda_max_cost

@@ -161,7 +161,7 @@ def main():
         ev[f"{name}_cost_g"] = np.array(cg, np.float32)
     np.savez_compressed(os.path.join(OUT, "ref_eval_n50.npz"), **ev)
 
-    # ---- first GD iterations (optimizer_GD.py:281-310, single loop) from alpha0
+    # ---- first GD iterations (optimizer_GD.py:68-97, single loop) from alpha0
     gd = {}
     for k in range(1, 6):
         args = ref_args(refmain, n_timesteps=N, optimizer_name="gd", max_outer_iteration=1, max_inner_iteration=k,

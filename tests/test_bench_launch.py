@@ -1,0 +1,40 @@
+"""bench.py's multi-rank launcher on CPU (no device): `bench.py --gpus 2` outside torchrun starts two
+ranks under torch.distributed.run itself and relays rank 0's JSON line.  `--dry-run`
+runs the launcher, the shard split, the environment broadcast and the max-time / Σ-iteration reduction
+without touching a GPU; tests/test_gpu_widen.py runs the same launcher with the kernels on the GPU box."""
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*argv):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *argv], stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, env=env, timeout=300, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+def test_gpus_flag_launches_ranks():
+    r = _bench("--gpus", "2", "--dry-run", "--max-inner", "200")
+    assert r["n_gpus"] == 2
+    assert r["config"]["global_batch"] == 2048 and r["config"]["batch_per_gpu"] == 1024
+    assert r["iterations_all"] == 2 * 1024 * 200  # Σ over ranks
+    assert r["elapsed_max"] == 2.0  # max over ranks (rank r reports 1 + r)
+    assert r["obstacles_equal_rank0"]  # rank 1 started with shifted obstacles and received rank 0's
+    c0, c1 = r["shard_checksums"]
+    assert c0 != c1  # disjoint shards of the global batch
+
+
+def test_single_rank_default():
+    r = _bench("--dry-run", "--config", "c5")
+    assert r["n_gpus"] == 1 and r["config"]["global_batch"] == 512
+    # bench-mode deviations from main.py's defaults are recorded in the config
+    ov = r["config"]["overrides_vs_reference_defaults"]
+    assert ov["gd_lr"] == [1e-3] and ov["max_outer_iteration"] == 1
+    assert r["config"]["gd_lr_first"] == 1e-3

@@ -268,3 +268,22 @@ def test_main_cli_two_ranks_sharded(tmp_path):
     np.testing.assert_allclose(b, a, rtol=0, atol=1e-4)
     sa, sb = np.loadtxt(d1 / batch_io.SUMMARY_BATCH), np.loadtxt(d2 / batch_io.SUMMARY_BATCH)
     np.testing.assert_array_equal(sa[:, 2:], sb[:, 2:])  # flags and iteration counts
+
+
+def test_bench_gpus_flag_runs_ranks():
+    """`bench.py --gpus 2` outside torchrun launches two ranks itself and reports n_gpus = 2 with the
+    whole job's iterations (the ranks share the box's one GPU, gloo collectives on host tensors); the
+    CPU baseline is kept on rank 0 at every world size."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+                        "--steps", "2", "--warmup", "1", "--max-inner", "20"], stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, text=True, env=env, timeout=300, cwd=repo)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert r["n_gpus"] == 2 and r["config"]["global_batch"] == 2048
+    assert r["iterations_per_step"] == 2 * 1024 * 20
+    assert r["value"] > 0 and r["cpu_baseline"]["value"] > 0

@@ -104,7 +104,7 @@ def test_init_trajectory(g_eval):
 
 
 def test_gd_first_iterations(g_gd):
-    """optimizer_GD.py:281-310 (jit_optimize): k = 1..5 steps from the same α0, atol 1e-3."""
+    """optimizer_GD.py:68-97 (jit_optimize): k = 1..5 steps from the same α0, atol 1e-3."""
     for k in range(1, 6):
         o = oracle_for("--optimizer-name", "gd", "--max-outer-iteration", 1, "--max-inner-iteration", k)
         al, st = o.optimize(g_gd["alpha0"], obstacles(), START, GOAL)
@@ -264,3 +264,22 @@ def test_oracle_whole_robot_cost_and_grad(g_wr, g_eval, name):
         assert np.abs(G - Gref).max() <= gtol * np.abs(Gref).max(), (lm, np.abs(G - Gref).max())
     # the end-effector cost is one of the summands: whole robot ≥ end effector
     assert o.cost(a, obs, START, GOAL, 0, 0, 0.0) > oracle_for().cost(a, obs, START, GOAL, 0, 0, 0.0)
+
+
+def test_oracle_outer_iteration_edge_cases():
+    """max_outer_iteration <= 1 for GD is the single loop (dualOptimization = max_outer > 1,
+    optimizer_GD.py:18, 54-65); for BLS <= 0 the outer while_loop never runs and α0 comes back
+    (optimizer_BLS.py:184-186, 210-213)."""
+    from conftest import obstacles, oracle_for
+    gd = ["--optimizer-name", "gd", "--max-inner-iteration", 7, "--loop-loss-reduction=-1e30"]
+    o1 = oracle_for(*gd, "--max-outer-iteration", 1)
+    o0 = oracle_for(*gd, "--max-outer-iteration", 0)
+    a0 = o1.init_alpha(START, GOAL)
+    a1, s1 = o1.optimize(a0, obstacles(), START, GOAL)
+    b1, t1 = o0.optimize(a0, obstacles(), START, GOAL)
+    np.testing.assert_array_equal(a1, b1)
+    assert s1["grad_evals"] == t1["grad_evals"] == 7
+    ob = oracle_for("--max-outer-iteration", 0)
+    a, st = ob.optimize(a0, obstacles(), START, GOAL)
+    np.testing.assert_array_equal(a, a0)
+    assert st["grad_evals"] == 0 and st["outer_iterations"] == 0
