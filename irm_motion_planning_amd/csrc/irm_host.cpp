@@ -24,6 +24,18 @@
 using irm::KParams;
 
 namespace {
+/* A hyper-parameter the reference holds as a Python double (argparse) reaches this library as a
+   float: recover the double the decimal argument denotes — the shortest decimal that round-trips the
+   float (0.1f → "0.1" → 0.1) — so derived constants such as fp32(2·σ²) round as the reference's do
+   (trajectory.py:14-19: 2*rbf_var**2 is a double, weakly typed to fp32 in the division). */
+double decimal_double(float f) {
+    char buf[32];
+    for (int prec = 6; prec <= 9; ++prec) {
+        snprintf(buf, sizeof buf, "%.*g", prec, (double)f);
+        if (strtof(buf, nullptr) == f) return strtod(buf, nullptr);
+    }
+    return (double)f;
+}
 
 thread_local std::string g_err;
 
@@ -85,34 +97,95 @@ void jacobi_eigen(std::vector<double>& a, int n, std::vector<double>& v) {
     }
 }
 
-// fp32 LU with partial pivoting; solves A·X = B (n×n, nrhs columns, row-major).
-// fp32 on purpose: trajectory.py:77 solves the singular K in fp32 (|α|≈1e3).
-bool lu_solve_f32(int n, const float* A_in, const float* B_in, int nrhs, float* X) {
-    std::vector<float> A(A_in, A_in + (size_t)n * n), B(B_in, B_in + (size_t)n * nrhs);
-    for (int k = 0; k < n; ++k) {
-        int p = k;
-        for (int i = k + 1; i < n; ++i)
-            if (fabsf(A[(size_t)i * n + k]) > fabsf(A[(size_t)p * n + k])) p = i;
-        if (A[(size_t)p * n + k] == 0.f) return false;
-        if (p != k) {
-            for (int j = 0; j < n; ++j) std::swap(A[(size_t)k * n + j], A[(size_t)p * n + j]);
-            for (int j = 0; j < nrhs; ++j) std::swap(B[(size_t)k * nrhs + j], B[(size_t)p * nrhs + j]);
+/* fp32 LU with partial pivoting in LAPACK's recursive order (sgetrf2: factor the left half of the
+   columns, swap, triangular solve, Schur update, factor the right half) followed by sgetrs's
+   substitutions.  numpy.linalg.solve — what trajectory.py:77 runs — is LAPACK sgesv; K is
+   numerically singular (cond ≈ 1e19), so α0's null-space part is rounding noise whose size depends
+   on the elimination order: the recursive order keeps |α0| at the reference's ~1e3 where the
+   right-looking textbook loop reached 4e4 (N=50), with K·α0·J within 3e-4 of the reference's. */
+void getrf2_f32(int m, int n, float* A, int lda, int* ipiv) {
+    if (n == 1) {
+        int p = 0;
+        for (int i = 1; i < m; ++i)
+            if (fabsf(A[(size_t)i * lda]) > fabsf(A[(size_t)p * lda])) p = i;
+        ipiv[0] = p;
+        if (p != 0) {
+            float t = A[0];
+            A[0] = A[(size_t)p * lda];
+            A[(size_t)p * lda] = t;
         }
-        const float piv = A[(size_t)k * n + k];
-        for (int i = k + 1; i < n; ++i) {
-            const float l = A[(size_t)i * n + k] / piv;
-            A[(size_t)i * n + k] = l;
-            for (int j = k + 1; j < n; ++j) A[(size_t)i * n + j] -= l * A[(size_t)k * n + j];
-            for (int j = 0; j < nrhs; ++j) B[(size_t)i * nrhs + j] -= l * B[(size_t)k * nrhs + j];
+        if (A[0] != 0.f) {
+            const float r = 1.f / A[0]; /* LAPACK scales by the reciprocal */
+            for (int i = 1; i < m; ++i) A[(size_t)i * lda] *= r;
+        }
+        return;
+    }
+    const int n1 = (m < n ? m : n) / 2, n2 = n - n1;
+    getrf2_f32(m, n1, A, lda, ipiv);
+    for (int i = 0; i < n1; ++i) /* row swaps of the left panel on the right columns */
+        if (ipiv[i] != i)
+            for (int j = n1; j < n; ++j) {
+                float t = A[(size_t)i * lda + j];
+                A[(size_t)i * lda + j] = A[(size_t)ipiv[i] * lda + j];
+                A[(size_t)ipiv[i] * lda + j] = t;
+            }
+    for (int i = 1; i < n1; ++i) /* A12 = L11⁻¹·A12 (unit lower) */
+        for (int k = 0; k < i; ++k) {
+            const float l = A[(size_t)i * lda + k];
+            for (int j = n1; j < n; ++j) A[(size_t)i * lda + j] -= l * A[(size_t)k * lda + j];
+        }
+    for (int i = n1; i < m; ++i) /* A22 −= A21·A12 */
+        for (int j = n1; j < n; ++j) {
+            float s = 0.f;
+            for (int k = 0; k < n1; ++k) s += A[(size_t)i * lda + k] * A[(size_t)k * lda + j];
+            A[(size_t)i * lda + j] -= s;
+        }
+    getrf2_f32(m - n1, n2, A + (size_t)n1 * lda + n1, lda, ipiv + n1);
+    for (int i = n1; i < (m < n ? m : n); ++i) {
+        ipiv[i] += n1;
+        if (ipiv[i] != i) /* the right factorisation's swaps on the left columns */
+            for (int j = 0; j < n1; ++j) {
+                float t = A[(size_t)i * lda + j];
+                A[(size_t)i * lda + j] = A[(size_t)ipiv[i] * lda + j];
+                A[(size_t)ipiv[i] * lda + j] = t;
+            }
+    }
+}
+
+/* A·X = B, A n×n, B / X n×nrhs, row-major; returns false if a pivot is exactly 0. */
+bool lu_solve_f32(int n, const float* A_in, const float* B_in, int nrhs, float* X) {
+    float* A = (float*)malloc(sizeof(float) * (size_t)n * n);
+    int* ipiv = (int*)malloc(sizeof(int) * (size_t)n);
+    bool ok = true;
+    memcpy(A, A_in, sizeof(float) * (size_t)n * n);
+    memcpy(X, B_in, sizeof(float) * (size_t)n * nrhs);
+    getrf2_f32(n, n, A, n, ipiv);
+    for (int i = 0; i < n; ++i) {
+        if (A[(size_t)i * n + i] == 0.f) ok = false;
+        if (ipiv[i] != i)
+            for (int j = 0; j < nrhs; ++j) {
+                float t = X[(size_t)i * nrhs + j];
+                X[(size_t)i * nrhs + j] = X[(size_t)ipiv[i] * nrhs + j];
+                X[(size_t)ipiv[i] * nrhs + j] = t;
+            }
+    }
+    if (ok) {
+        for (int j = 0; j < nrhs; ++j) {
+            for (int i = 1; i < n; ++i) {
+                float s = X[(size_t)i * nrhs + j];
+                for (int k = 0; k < i; ++k) s -= A[(size_t)i * n + k] * X[(size_t)k * nrhs + j];
+                X[(size_t)i * nrhs + j] = s;
+            }
+            for (int i = n - 1; i >= 0; --i) {
+                float s = X[(size_t)i * nrhs + j];
+                for (int k = i + 1; k < n; ++k) s -= A[(size_t)i * n + k] * X[(size_t)k * nrhs + j];
+                X[(size_t)i * nrhs + j] = s / A[(size_t)i * n + i];
+            }
         }
     }
-    for (int j = 0; j < nrhs; ++j)
-        for (int i = n - 1; i >= 0; --i) {
-            float s = B[(size_t)i * nrhs + j];
-            for (int k = i + 1; k < n; ++k) s -= A[(size_t)i * n + k] * X[(size_t)k * nrhs + j];
-            X[(size_t)i * nrhs + j] = s / A[(size_t)i * n + i];
-        }
-    return true;
+    free(A);
+    free(ipiv);
+    return ok;
 }
 
 // ------------------------------------------------ legacy threefry (J)
@@ -382,7 +455,7 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
     c->K.resize((size_t)N * N);
     c->dK.resize((size_t)N * N);
     {
-        const double sig = p->rbf_variance;
+        const double sig = decimal_double(p->rbf_variance);
         const float two_s2 = (float)(2.0 * sig * sig), s2 = (float)(sig * sig);
         for (int i = 0; i < N; ++i)
             for (int j = 0; j < N; ++j) {

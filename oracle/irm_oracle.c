@@ -1,3 +1,4 @@
+#include <stdio.h>
 /*
  * irm_oracle.c — plain-C fp32 restatement of the reference's α-space
  * optimiser.  TEST INFRASTRUCTURE ONLY (see irm_oracle.h).
@@ -15,6 +16,19 @@
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
+
+/* A hyper-parameter the reference holds as a Python double (argparse) reaches this library as a
+   float: recover the double the decimal argument denotes — the shortest decimal that round-trips the
+   float (0.1f → "0.1" → 0.1) — so derived constants such as fp32(2·σ²) round as the reference's do
+   (trajectory.py:14-19: 2*rbf_var**2 is a double, weakly typed to fp32 in the division). */
+static double decimal_double(float f) {
+    char buf[32];
+    for (int prec = 6; prec <= 9; ++prec) {
+        snprintf(buf, sizeof buf, "%.*g", prec, (double)f);
+        if (strtof(buf, NULL) == f) return strtod(buf, NULL);
+    }
+    return (double)f;
+}
 #endif
 
 struct orc_ctx {
@@ -59,7 +73,7 @@ orc_ctx* orc_create(const irm_params* p) {
     /* trajectory.py:14-19,40-48: a,b = meshgrid(t,t) -> a[i][j]=t_j, b[i][j]=t_i;
        K = exp(-(a-b)^2/(2σ^2)), dK = (a-b)/σ^2 * exp(...). σ enters as a
        Python double: 2*rbf_var**2 and rbf_var**2 are doubles cast to fp32. */
-    double sig = p->rbf_variance;
+    double sig = decimal_double(p->rbf_variance);
     float two_s2 = (float)(2.0 * sig * sig), s2 = (float)(sig * sig);
     for (int i = 0; i < N; ++i)
         for (int j = 0; j < N; ++j) {
@@ -503,36 +517,95 @@ int32_t orc_constraints(const orc_ctx* c, const float* alpha, const float* s, co
     return constraints_traj(c, traj, vel, s, g, report);
 }
 
-/* fp32 LU with partial pivoting (row-major, right-looking), then solve. */
-static void lu_solve(int n, const float* A_in, const float* B_in, float* X, int nrhs) {
-    float* A = (float*)malloc(sizeof(float) * n * n);
-    float* B = (float*)malloc(sizeof(float) * n * nrhs);
-    memcpy(A, A_in, sizeof(float) * n * n);
-    memcpy(B, B_in, sizeof(float) * n * nrhs);
-    for (int k = 0; k < n; ++k) {
-        int p = k;
-        for (int i = k + 1; i < n; ++i)
-            if (fabsf(A[i * n + k]) > fabsf(A[p * n + k])) p = i;
-        if (p != k) {
-            for (int j = 0; j < n; ++j) { float t = A[k * n + j]; A[k * n + j] = A[p * n + j]; A[p * n + j] = t; }
-            for (int j = 0; j < nrhs; ++j) { float t = B[k * nrhs + j]; B[k * nrhs + j] = B[p * nrhs + j]; B[p * nrhs + j] = t; }
+/* fp32 LU with partial pivoting in LAPACK's recursive order (sgetrf2: factor the left half of the
+   columns, swap, triangular solve, Schur update, factor the right half) followed by sgetrs's
+   substitutions.  numpy.linalg.solve — what trajectory.py:77 runs — is LAPACK sgesv; K is
+   numerically singular (cond ≈ 1e19), so α0's null-space part is rounding noise whose size depends
+   on the elimination order: the recursive order keeps |α0| at the reference's ~1e3 where the
+   right-looking textbook loop reached 4e4 (N=50), with K·α0·J within 3e-4 of the reference's. */
+static void getrf2_f32(int m, int n, float* A, int lda, int* ipiv) {
+    if (n == 1) {
+        int p = 0;
+        for (int i = 1; i < m; ++i)
+            if (fabsf(A[(size_t)i * lda]) > fabsf(A[(size_t)p * lda])) p = i;
+        ipiv[0] = p;
+        if (p != 0) {
+            float t = A[0];
+            A[0] = A[(size_t)p * lda];
+            A[(size_t)p * lda] = t;
         }
-        float piv = A[k * n + k];
-        for (int i = k + 1; i < n; ++i) {
-            float l = A[i * n + k] / piv;
-            A[i * n + k] = l;
-            for (int j = k + 1; j < n; ++j) A[i * n + j] -= l * A[k * n + j];
-            for (int j = 0; j < nrhs; ++j) B[i * nrhs + j] -= l * B[k * nrhs + j];
+        if (A[0] != 0.f) {
+            const float r = 1.f / A[0]; /* LAPACK scales by the reciprocal */
+            for (int i = 1; i < m; ++i) A[(size_t)i * lda] *= r;
+        }
+        return;
+    }
+    const int n1 = (m < n ? m : n) / 2, n2 = n - n1;
+    getrf2_f32(m, n1, A, lda, ipiv);
+    for (int i = 0; i < n1; ++i) /* row swaps of the left panel on the right columns */
+        if (ipiv[i] != i)
+            for (int j = n1; j < n; ++j) {
+                float t = A[(size_t)i * lda + j];
+                A[(size_t)i * lda + j] = A[(size_t)ipiv[i] * lda + j];
+                A[(size_t)ipiv[i] * lda + j] = t;
+            }
+    for (int i = 1; i < n1; ++i) /* A12 = L11⁻¹·A12 (unit lower) */
+        for (int k = 0; k < i; ++k) {
+            const float l = A[(size_t)i * lda + k];
+            for (int j = n1; j < n; ++j) A[(size_t)i * lda + j] -= l * A[(size_t)k * lda + j];
+        }
+    for (int i = n1; i < m; ++i) /* A22 −= A21·A12 */
+        for (int j = n1; j < n; ++j) {
+            float s = 0.f;
+            for (int k = 0; k < n1; ++k) s += A[(size_t)i * lda + k] * A[(size_t)k * lda + j];
+            A[(size_t)i * lda + j] -= s;
+        }
+    getrf2_f32(m - n1, n2, A + (size_t)n1 * lda + n1, lda, ipiv + n1);
+    for (int i = n1; i < (m < n ? m : n); ++i) {
+        ipiv[i] += n1;
+        if (ipiv[i] != i) /* the right factorisation's swaps on the left columns */
+            for (int j = 0; j < n1; ++j) {
+                float t = A[(size_t)i * lda + j];
+                A[(size_t)i * lda + j] = A[(size_t)ipiv[i] * lda + j];
+                A[(size_t)ipiv[i] * lda + j] = t;
+            }
+    }
+}
+
+/* A·X = B, A n×n, B / X n×nrhs, row-major; returns 0 if a pivot is exactly 0. */
+static int lu_solve_f32(int n, const float* A_in, const float* B_in, int nrhs, float* X) {
+    float* A = (float*)malloc(sizeof(float) * (size_t)n * n);
+    int* ipiv = (int*)malloc(sizeof(int) * (size_t)n);
+    int ok = 1;
+    memcpy(A, A_in, sizeof(float) * (size_t)n * n);
+    memcpy(X, B_in, sizeof(float) * (size_t)n * nrhs);
+    getrf2_f32(n, n, A, n, ipiv);
+    for (int i = 0; i < n; ++i) {
+        if (A[(size_t)i * n + i] == 0.f) ok = 0;
+        if (ipiv[i] != i)
+            for (int j = 0; j < nrhs; ++j) {
+                float t = X[(size_t)i * nrhs + j];
+                X[(size_t)i * nrhs + j] = X[(size_t)ipiv[i] * nrhs + j];
+                X[(size_t)ipiv[i] * nrhs + j] = t;
+            }
+    }
+    if (ok) {
+        for (int j = 0; j < nrhs; ++j) {
+            for (int i = 1; i < n; ++i) {
+                float s = X[(size_t)i * nrhs + j];
+                for (int k = 0; k < i; ++k) s -= A[(size_t)i * n + k] * X[(size_t)k * nrhs + j];
+                X[(size_t)i * nrhs + j] = s;
+            }
+            for (int i = n - 1; i >= 0; --i) {
+                float s = X[(size_t)i * nrhs + j];
+                for (int k = i + 1; k < n; ++k) s -= A[(size_t)i * n + k] * X[(size_t)k * nrhs + j];
+                X[(size_t)i * nrhs + j] = s / A[(size_t)i * n + i];
+            }
         }
     }
-    for (int j = 0; j < nrhs; ++j)
-        for (int i = n - 1; i >= 0; --i) {
-            float s = B[i * nrhs + j];
-            for (int k = i + 1; k < n; ++k) s -= A[i * n + k] * X[k * nrhs + j];
-            X[i * nrhs + j] = s / A[i * n + i];
-        }
     free(A);
-    free(B);
+    free(ipiv);
+    return ok;
 }
 
 /* trajectory.py:73-78: α0 = solve(K, (s + (g-s) c) @ inv(J)). */
@@ -543,13 +616,13 @@ void orc_init_alpha(const orc_ctx* c, const float* s, const float* g, float* alp
     float Jl[IRM_MAX_JOINTS * IRM_MAX_JOINTS];
     for (int i = 0; i < D; ++i)
         for (int j = 0; j < D; ++j) Jl[i * D + j] = c->J[i * D + j];
-    lu_solve(D, Jl, eye, Jinv, D);
+    lu_solve_f32(D, Jl, eye, D, Jinv);
     float* line = (float*)malloc(sizeof(float) * N * D);
     float* rhs = (float*)malloc(sizeof(float) * N * D);
     for (int n = 0; n < N; ++n)
         for (int k = 0; k < D; ++k) line[n * D + k] = s[k] + (g[k] - s[k]) * c->c[n];
     matmul(line, Jinv, rhs, N, D, D);
-    lu_solve(N, c->K, rhs, alpha_out, D);
+    lu_solve_f32(N, c->K, rhs, D, alpha_out);
     free(line);
     free(rhs);
 }
@@ -609,8 +682,27 @@ static void optimize_gd(const orc_ctx* c, float* alpha, const float* obs, int O,
 }
 
 /* optimizer_BLS.py:126-213 (jit_optimize). */
+/* Line-search log (tests): per trial ORC_TRACE_W floats — outer, inner, trial, lr, new_loss,
+   required_loss, accepted, loss, ‖g‖, alpha_norm (optimizer_BLS.py:139-149, 163-166). */
+typedef struct {
+    float* buf;
+    int32_t cap, n;
+} bls_trace;
+
+static void trace_put(bls_trace* tr, int outer, int inner, int trial, float lr, float nl, float req, int acc,
+                      float loss, float gn, float an) {
+    if (!tr || !tr->buf || tr->n >= tr->cap) {
+        if (tr) tr->n++;
+        return;
+    }
+    float* r = tr->buf + (size_t)tr->n * ORC_TRACE_W;
+    r[0] = (float)outer; r[1] = (float)inner; r[2] = (float)trial; r[3] = lr; r[4] = nl; r[5] = req;
+    r[6] = (float)acc; r[7] = loss; r[8] = gn; r[9] = an;
+    tr->n++;
+}
+
 static void optimize_bls(const orc_ctx* c, float* alpha, const float* obs, int O, const float* s,
-                         const float* g, irm_stats* st, float* series, int32_t max_series) {
+                         const float* g, irm_stats* st, float* series, int32_t max_series, bls_trace* trc) {
     const irm_params* p = &c->p;
     int N = c->N, D = c->D, ND = N * D;
     float lsg = p->lambda_sg_constraint, ljl = p->lambda_jl_constraint;
@@ -646,6 +738,7 @@ static void optimize_bls(const orc_ctx* c, float* alpha, const float* obs, int O
                 st->cost_evals++;
                 st->bls_trials++;
                 float required = loss - p->bls_alpha * lr * anorm;
+                trace_put(trc, outer, it, j, lr, nl, required, !(nl > required), loss, nrm, anorm);
                 if (nl > required) {
                     lr = lr * p->bls_beta_minus;
                 } else {
@@ -683,17 +776,25 @@ static void optimize_bls(const orc_ctx* c, float* alpha, const float* obs, int O
     st->constraints_ok = fulfilled;
 }
 
-void orc_optimize(const orc_ctx* c, const float* alpha0, const float* obstacles, int32_t O, const float* s,
-                  const float* g, float* alpha_out, irm_stats* stats, float* series, int32_t max_series) {
+int32_t orc_optimize_trace(const orc_ctx* c, const float* alpha0, const float* obstacles, int32_t O, const float* s,
+                           const float* g, float* alpha_out, irm_stats* stats, float* series, int32_t max_series,
+                           float* trace, int32_t trace_cap) {
     irm_stats st;
     memset(&st, 0, sizeof(st));
+    bls_trace tr = {trace, trace_cap, 0};
     memcpy(alpha_out, alpha0, sizeof(float) * c->N * c->D);
     snapshot(c, alpha_out, series, max_series, &st.series_len); /* row 0 = initial trajectory */
     if (c->p.optimizer == IRM_OPT_BLS)
-        optimize_bls(c, alpha_out, obstacles, O, s, g, &st, series, max_series);
+        optimize_bls(c, alpha_out, obstacles, O, s, g, &st, series, max_series, &tr);
     else
         optimize_gd(c, alpha_out, obstacles, O, s, g, &st, series, max_series);
     if (stats) *stats = st;
+    return tr.n;
+}
+
+void orc_optimize(const orc_ctx* c, const float* alpha0, const float* obstacles, int32_t O, const float* s,
+                  const float* g, float* alpha_out, irm_stats* stats, float* series, int32_t max_series) {
+    (void)orc_optimize_trace(c, alpha0, obstacles, O, s, g, alpha_out, stats, series, max_series, NULL, 0);
 }
 
 void orc_optimize_batch(const orc_ctx* c, const float* alpha0, const float* start, const float* goal,

@@ -46,6 +46,14 @@ void orc_init_alpha(const orc_ctx* c, const float* s, const float* g, float* alp
 void orc_optimize(const orc_ctx* c, const float* alpha0, const float* obstacles, int32_t O, const float* s,
                   const float* g, float* alpha_out, irm_stats* stats, float* series, int32_t max_series);
 
+/* orc_optimize plus the BLS line-search log: ORC_TRACE_W floats per trial (outer, inner, trial, lr,
+ * new_loss, required_loss, accepted, loss, ‖g‖, alpha_norm), at most trace_cap records; returns the
+ * number of trials (may exceed trace_cap). */
+#define ORC_TRACE_W 10
+int32_t orc_optimize_trace(const orc_ctx* c, const float* alpha0, const float* obstacles, int32_t O, const float* s,
+                           const float* g, float* alpha_out, irm_stats* stats, float* series, int32_t max_series,
+                           float* trace, int32_t trace_cap);
+
 /* Batch driver (OpenMP over trajectories; n_threads <= 0: all). */
 void orc_optimize_batch(const orc_ctx* c, const float* alpha0, const float* start, const float* goal,
                         const float* obstacles, int32_t O, int32_t obstacle_stride, int32_t B,

@@ -50,6 +50,9 @@ def _load():
         lib.orc_constraints.restype = ctypes.c_int32
         lib.orc_constraints.argtypes = [ctypes.c_void_p, _fp, _fp, _fp, _fp]
         lib.orc_init_alpha.argtypes = [ctypes.c_void_p, _fp, _fp, _fp]
+        lib.orc_optimize_trace.restype = ctypes.c_int32
+        lib.orc_optimize_trace.argtypes = [ctypes.c_void_p, _fp, _fp, ctypes.c_int32, _fp, _fp, _fp,
+                                           ctypes.POINTER(IrmStats), _fp, ctypes.c_int32, _fp, ctypes.c_int32]
         lib.orc_optimize.argtypes = [ctypes.c_void_p, _fp, _fp, ctypes.c_int32, _fp, _fp, _fp,
                                      ctypes.POINTER(IrmStats), _fp, ctypes.c_int32]
         lib.orc_optimize_batch.argtypes = [ctypes.c_void_p, _fp, _fp, _fp, _fp, ctypes.c_int32, ctypes.c_int32,
@@ -161,6 +164,17 @@ class Oracle:
         if max_series:
             return out, res, series[: st.series_len]
         return out, res
+
+    def optimize_trace(self, alpha0, obstacles, s, g, cap=256):
+        """optimize() plus the BLS line-search log: rows (outer, inner, trial, lr, new_loss,
+        required_loss, accepted, loss, |g|, alpha_norm)."""
+        obs = _f(obstacles)
+        out = np.zeros((self.N, self.D), np.float32)
+        st = IrmStats()
+        tr = np.zeros((cap, 10), np.float32)
+        n = _load().orc_optimize_trace(self._c, _p(_f(alpha0)), _p(obs), obs.shape[0], _p(_f(s)), _p(_f(g)), _p(out),
+                                   ctypes.byref(st), None, 0, _p(tr), cap)
+        return out, stats_dict(st), tr[:min(n, cap)]
 
     def optimize_batch(self, alpha0, start, goal, obstacles, obstacle_stride=0, n_threads=0):
         start = _f(start)

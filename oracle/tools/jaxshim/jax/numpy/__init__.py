@@ -5,12 +5,16 @@ TEST INFRASTRUCTURE ONLY (see ../__init__.py).  Mirrors JAX's default
 result int32, int32 arrays combined with floats promote to float32 (not
 float64 as plain numpy would), and arrays support `.at[idx].set(v)`.
 Set IRM_JAXSHIM_X64=1 to compute in float64 instead (finite-difference checks).
+Set IRM_JAXSHIM_MATMUL=exact to accumulate every `@` (matmul) in float64 and round the result
+once to float32 — the correctly rounded contraction the build's kernels and C oracle use — while
+every other operation keeps the reference's fp32 arithmetic (gen_golden_bench.py's "_xm" fixtures).
 """
 import os
 
 import numpy as _np
 
 _X64 = os.environ.get("IRM_JAXSHIM_X64", "0") == "1"
+_XMATMUL = os.environ.get("IRM_JAXSHIM_MATMUL", "") == "exact"
 FLOAT = _np.float64 if _X64 else _np.float32
 INT = _np.int64 if _X64 else _np.int32
 
@@ -88,6 +92,9 @@ class JArray(_np.ndarray):
 
     def __array_ufunc__(self, ufunc, method, *inputs, **kwargs):
         args = [_plain(a) for a in inputs]
+        if _XMATMUL and ufunc is _np.matmul and method == "__call__":
+            args = [a.astype(_np.float64) if isinstance(a, _np.ndarray) else a for a in _promote(args)]
+            return _canon(_np.matmul(*args).astype(FLOAT))
         if ufunc not in (_np.logical_and, _np.logical_or, _np.logical_not, _np.invert):
             args = _promote(args)
         kwargs.pop("out", None)

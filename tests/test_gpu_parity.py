@@ -16,7 +16,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import E2E_CASES, GOAL, START, check_quality, obstacles, oracle_for, params
+from conftest import E2E_CASES, GOAL, START, check_iterations, check_quality, obstacles, oracle_for, params
 
 pytestmark = pytest.mark.gpu
 
@@ -224,19 +224,31 @@ def test_gd_single_loop_iteration_count(g_gd):
     assert int(st["grad_evals"]) == 128
 
 
-@pytest.mark.parametrize("tag", sorted(E2E_CASES))
+def _e2e_cases():
+    from test_reference_bench import E2E_R02, e2e_obstacles
+    cases = {t: (a, obstacles(n)) for t, (a, n) in E2E_CASES.items()}
+    cases.update({t: (a, e2e_obstacles(src)) for t, (a, src) in E2E_R02.items()})
+    return cases
+
+
+@pytest.mark.parametrize("tag", sorted(list(E2E_CASES) + ["gd_n50_lmax0.0", "gd_n50_lmax0.25", "gd_n50_lmax0.75",
+                                                         "gd_n50_lmax1.0", "gd_n128", "gd_n256", "bls_n256_c4obs"]))
 @pytest.mark.parametrize("rank", [0, -1])
-def test_end_to_end_quality(g_e2e, tag, rank):
-    """Full optimize() at the reference defaults, low-rank (auto) and dense operator."""
-    argv, n_obs = E2E_CASES[tag]
+def test_end_to_end_quality(tag, rank):
+    """Full optimize() at the reference defaults (reference control flow), low-rank (auto) and dense
+    operator: quality and flag inside the reference's outcomes, inner iterations inside ±30 % of the
+    reference with correctly rounded matmuls (conftest.check_quality / check_iterations)."""
+    argv, obs = _e2e_cases()[tag]
+    if rank == -1 and "n256" in tag:
+        pytest.skip("dense operator at N=256: covered at N <= 128")
     c = ctx(*argv, operator_rank=rank)
-    obs = obstacles(n_obs)
     alpha, traj, st = c.optimize(START, GOAL, obs)
     avg = c.eval_cost(alpha, obs, START, GOAL, 0, 0, 0)
     mx = c.eval_cost(alpha, obs, START, GOAL, 0, 0, 1)
-    ok, _ = c.constraints(alpha, START, GOAL)
+    ok, rep = c.constraints(alpha, START, GOAL)
     assert bool(st["constraints_ok"]) == ok
-    check_quality(g_e2e, tag, avg, mx, ok)
+    check_quality(tag, avg, mx, ok, rep)
+    check_iterations(tag, st["grad_evals"])
     np.testing.assert_allclose(c.evaluate(alpha), traj, rtol=0, atol=2e-3)
 
 
@@ -507,7 +519,7 @@ def test_object_api(g_e2e):
         avg = tr.compute_trajectory_cost(alpha, env.obstacles, env.start_config, env.goal_config, 0, 0, 0)
         mx = tr.compute_trajectory_cost(alpha, env.obstacles, env.start_config, env.goal_config, 0, 0, 1)
         ok = tr.constraintsFulfilledVerbose(alpha, env.start_config, env.goal_config, verbose=False)
-        check_quality(g_e2e, tag, avg, mx, ok)
+        check_quality(tag, avg, mx, ok)
         traj = tr.evaluate(alpha, tr.km, tr.jac)
         assert traj.shape == (50, 3)
         g = tr.compute_trajectory_cost_g(alpha, env.obstacles, env.start_config, env.goal_config, 0.5, 0.1, 0.5)

@@ -1,0 +1,170 @@
+"""The C oracle against reference-produced fixtures at the bench shapes (CPU).
+
+tests/golden/ref_bench_c3.npz / ref_bench_c4.npz / ref_bls_trials.npz / ref_e2e_r02.npz come from the
+unmodified reference (oracle/tools/gen_golden_bench.py through the jax adapter):
+
+  * C3 (BASELINE configs[2]: N=128, the reference's 11 obstacles, bench.make_problem("c3") problems)
+    and C4 (N=256, 50 random obstacles): GD single loop in bench mode from the reference's α0 —
+    the 1..5-step trajectories, the 200-step trajectory and loss, and the same run from α0 ± 1 ulp;
+  * the BLS line search of the first inner iterations (optimizer_BLS.py:135-179): per trial lr,
+    new_loss, required_loss and accept, per iteration loss, ‖g‖, alpha_norm;
+  * reference control flow end to end (GD λ_max table, N=128 / 256) with ±1-ulp ensembles.
+
+Tolerances (shared with the GPU tests in test_gpu_reference.py):
+  * k ≤ 5 GD steps: waypoints within max(2·spread_k, 1e-3) (SURVEY.md §8c's 1e-3, widened to the
+    reference's own ±1-ulp sensitivity after k steps: at N=256 with 50 obstacles the fp32 noise of
+    K@α0 moves the first gradient's max-cost argmax and one step already spreads 3.5e-3), loss rtol
+    1e-3 (near α0 the reference's loss carries the fp32 noise of K@α0 in its start / goal terms);
+  * trajectories are compared as K·α·J of the reference's fp32 α in exact arithmetic (its own
+    evaluate adds the fp32 noise of K@α with |α| ≈ 1e3 on top: 1.5e-3 at N=128, 7e-3 at N=256);
+  * 200 GD steps: |traj − ref|∞ ≤ max(2·spread, 3e-3) with spread = the reference's own distance to its
+    ±1-ulp runs (max over members) — the reference iterates α in fp32 (|α| ≈ 1e3) and the result is
+    pinned to that rounding to within the fp32 noise of its K@α products;
+    final loss inside the ensemble's range ± 1e-3 relative;
+  * BLS trial log from a well-conditioned α: accept / reject sequence identical, lr exact, losses,
+    ‖g‖, alpha_norm rtol 1e-5; from the reference's α0 (singular solve, K@α0 carries fp32 noise of
+    ~5e-4 in waypoints and 1e-3 in velocities): sequence identical, lr exact, losses rtol 2e-3,
+    ‖g‖ 5e-3, alpha_norm 3e-2;
+  * end to end: conftest.check_quality (cost / flag inside the ensemble) and the gradient-call count
+    inside [0.7·min, 1.3·max] of the reference's ensemble (SURVEY.md §8c's ±30 %).
+"""
+import numpy as np
+import pytest
+
+from conftest import GOAL, START, check_iterations, check_quality, golden, oracle_for
+
+BENCH_ARGS = ("--optimizer-name", "gd", "--max-outer-iteration", 1, "--loop-loss-reduction=-1e30")
+
+
+def bench_band(spread):
+    return max(2.0 * spread, 3e-3)
+
+
+@pytest.fixture(scope="module")
+def g_c3():
+    return golden("ref_bench_c3")
+
+
+@pytest.fixture(scope="module")
+def g_c4():
+    return golden("ref_bench_c4")
+
+
+@pytest.fixture(scope="module")
+def g_bls():
+    return golden("ref_bls_trials")
+
+
+@pytest.fixture(scope="module")
+def g_e2e2():
+    return golden("ref_e2e_r02")
+
+
+def _n(z):
+    return int(z["traj_final"].shape[1])
+
+
+def exact_traj(o, alpha):
+    """K·α·J of the reference's fp32 α in exact arithmetic (the reference's own evaluate adds the fp32
+    noise of K@α, |α| ≈ 1e3: ~1.5e-3 at N=128, ~7e-3 at N=256 — not a property of its iteration)."""
+    _, K, _, J = o.kernel_matrices()
+    return np.asarray(K, np.float64) @ np.asarray(alpha, np.float64) @ np.asarray(J, np.float64)
+
+
+@pytest.mark.parametrize("cfg", ["c3", "c4"])
+def test_oracle_gd_first_steps(cfg, g_c3, g_c4):
+    z = g_c3 if cfg == "c3" else g_c4
+    N = _n(z)
+    for i, k in enumerate(z["ks"]):
+        o = oracle_for(*BENCH_ARGS, "--n-timesteps", N, "--max-inner-iteration", int(k))
+        for b in range(len(z["start"])):
+            al, st = o.optimize(z["alpha0"][b], z["obstacles"], z["start"][b], z["goal"][b])
+            assert st["grad_evals"] == k
+            ref = exact_traj(o, z["alpha_k"][b, i])
+            spread = max(float(np.abs(exact_traj(o, a) - ref).max()) for a in z["ens_alpha_k"][b, :, i])
+            err = float(np.abs(o.evaluate(al) - ref).max())
+            assert err <= max(2.0 * spread, 1e-3), (cfg, k, b, err, spread)
+            assert abs(st["final_loss"] - z["loss_k"][b, i]) <= 1e-3 * abs(z["loss_k"][b, i])
+
+
+@pytest.mark.parametrize("cfg", ["c3", "c4"])
+def test_oracle_gd_200_steps_inside_reference_spread(cfg, g_c3, g_c4):
+    z = g_c3 if cfg == "c3" else g_c4
+    o = oracle_for(*BENCH_ARGS, "--n-timesteps", _n(z), "--max-inner-iteration", int(z["steps"]))
+    for b in range(len(z["start"])):
+        al, st = o.optimize(z["alpha0"][b], z["obstacles"], z["start"][b], z["goal"][b])
+        ref = exact_traj(o, z["alpha_final"][b])
+        spread = max(float(np.abs(exact_traj(o, a) - ref).max()) for a in z["ens_alpha_final"][b])
+        err = float(np.abs(o.evaluate(al) - ref).max())
+        assert err <= bench_band(spread), (cfg, b, err, spread)
+        losses = np.append(z["ens_loss_final"][b], z["loss_final"][b])
+        tol = 1e-3 * abs(float(z["loss_final"][b]))
+        assert losses.min() - tol <= st["final_loss"] <= losses.max() + tol, (cfg, b, st["final_loss"], losses)
+
+
+BLS_CASES = [(N, kind) for N in (50, 128) for kind in ("wellcond", "alpha0")]
+BLS_TOL = {"wellcond": dict(loss=1e-5, gn=1e-5, an=1e-5), "alpha0": dict(loss=2e-3, gn=5e-3, an=3e-2)}
+
+
+def check_bls_log(trace, z, N, kind):
+    """trace rows (outer, inner, trial, lr, new_loss, required, accepted, loss, |g|, alpha_norm) against
+    the reference's line-search log (trials: inner, trial, lr, new_loss, required, accepted;
+    iterations: loss, |g|, alpha_norm)."""
+    pre = f"n{N}_{kind}__"
+    ref, its = z[pre + "trials"], z[pre + "iterations"]
+    tol = BLS_TOL[kind]
+    assert len(trace) == len(ref), (len(trace), len(ref))
+    np.testing.assert_array_equal(trace[:, 1], ref[:, 0])  # inner iteration of each trial
+    np.testing.assert_array_equal(trace[:, 2], ref[:, 1])  # trial index
+    np.testing.assert_array_equal(trace[:, 6].astype(int), ref[:, 5].astype(int))  # accept / reject
+    np.testing.assert_allclose(trace[:, 3], ref[:, 2], rtol=1e-7)  # lr
+    np.testing.assert_allclose(trace[:, 4], ref[:, 3], rtol=tol["loss"])  # new_loss
+    np.testing.assert_allclose(trace[:, 5], ref[:, 4], rtol=tol["loss"])  # required_loss
+    first = [int(np.where(trace[:, 1] == i)[0][0]) for i in range(len(its))]
+    np.testing.assert_allclose(trace[first, 7], its[:, 0], rtol=tol["loss"])  # loss at α
+    np.testing.assert_allclose(trace[first, 8], its[:, 1], rtol=tol["gn"])  # ‖g‖
+    np.testing.assert_allclose(trace[first, 9], its[:, 2], rtol=tol["an"])  # alpha_norm
+
+
+BLS_LOG_ARGS = ("--max-inner-iteration", 4, "--max-outer-iteration", 1, "--loop-loss-reduction=-1e30")
+
+
+@pytest.mark.parametrize("N,kind", BLS_CASES)
+def test_oracle_bls_line_search_log(g_bls, N, kind):
+    pre = f"n{N}_{kind}__"
+    o = oracle_for("--n-timesteps", N, *BLS_LOG_ARGS)
+    _, _, tr = o.optimize_trace(g_bls[pre + "alpha_init"], g_bls[pre + "obstacles"], START, GOAL)
+    check_bls_log(tr, g_bls, N, kind)
+
+
+# reference control flow (main.py defaults): tag -> (argv, obstacles source)
+E2E_R02 = {
+    "gd_n50_lmax0.0": (["--optimizer-name", "gd", "--lambda-max-cost", "0.0"], None),
+    "gd_n50_lmax0.25": (["--optimizer-name", "gd", "--lambda-max-cost", "0.25"], None),
+    "gd_n50_lmax0.75": (["--optimizer-name", "gd", "--lambda-max-cost", "0.75"], None),
+    "gd_n50_lmax1.0": (["--optimizer-name", "gd", "--lambda-max-cost", "1.0"], None),
+    "gd_n128": (["--optimizer-name", "gd", "--n-timesteps", "128"], None),
+    "gd_n256": (["--optimizer-name", "gd", "--n-timesteps", "256"], None),
+    "bls_n256_c4obs": (["--n-timesteps", "256"], "c4"),
+}
+
+
+def e2e_obstacles(src):
+    from conftest import obstacles
+    if src is None:
+        return obstacles()
+    import bench
+    return bench.make_problem(src, 1, 0)[2]
+
+
+@pytest.mark.parametrize("tag", sorted(E2E_R02))
+def test_oracle_end_to_end_r02(g_e2e2, tag):
+    argv, src = E2E_R02[tag]
+    o = oracle_for(*argv)
+    obs = e2e_obstacles(src)
+    al, st = o.optimize(o.init_alpha(START, GOAL), obs, START, GOAL)
+    avg = o.cost(al, obs, START, GOAL, 0, 0, 0)
+    mx = o.cost(al, obs, START, GOAL, 0, 0, 1)
+    ok, rep = o.constraints(al, START, GOAL)
+    check_quality(tag, avg, mx, ok, rep)
+    check_iterations(tag, st["grad_evals"])
