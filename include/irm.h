@@ -228,6 +228,16 @@ int32_t irm_series_capacity(const irm_ctx* ctx);
  * the number of workgroups written. */
 int irm_debug_phase_profile(irm_ctx* ctx, uint64_t* out, int32_t max_blocks);
 
+/* Diagnostics: line-search log of problem 0 of every later BLS optimize on this
+ * context — one record of 10 floats per trial, the values optimizer_BLS.py
+ * computes at optimizer_BLS.py:139-149 (trial) and :163-166 (inner-loop head):
+ * outer, inner, trial, lr, new_loss, required_loss, accepted, loss, ‖g‖,
+ * alpha_norm.  cap records are kept (0 disables).  The record count of a run is
+ * that problem's irm_stats.bls_trials (at most cap are stored). */
+int irm_debug_bls_trace_enable(irm_ctx* ctx, int32_t cap);
+/* Copy up to cap records of the last run's log; returns the number copied. */
+int irm_debug_bls_trace(irm_ctx* ctx, float* out, int32_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -154,6 +154,8 @@ PROTOTYPES = {
     "irm_optimize_batch_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(IrmBatchDev), ctypes.c_void_p]),
     "irm_series_capacity": (ctypes.c_int32, [ctypes.c_void_p]),
     "irm_debug_phase_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32]),
+    "irm_debug_bls_trace_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
+    "irm_debug_bls_trace": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_int32]),
 }
 
 _LIB = None

@@ -216,6 +216,21 @@ class Context:
             return alpha, traj, st, ser
         return alpha, traj, st
 
+    def bls_trace_enable(self, cap=256):
+        """Record the line-search log of problem 0 of every later BLS optimize (diagnostics)."""
+        check(self.lib.irm_debug_bls_trace_enable(self._h, int(cap)))
+        self._trace_cap = int(cap)
+
+    def bls_trace(self, n_trials):
+        """The last run's log: n_trials × 10 (outer, inner, trial, lr, new_loss, required_loss,
+        accepted, loss, ‖g‖, alpha_norm) — optimizer_BLS.py:139-149, 163-166."""
+        cap = getattr(self, "_trace_cap", 0)
+        out = np.zeros((cap, 10), np.float32)
+        n = self.lib.irm_debug_bls_trace(self._h, _ptr(out), cap)
+        if n < 0:
+            check(n)
+        return out[: min(int(n_trials), n)]
+
     def optimize_dev(self, batch_dev, stream=0):
         """Enqueue irm_optimize_batch_dev with device pointers (IrmBatchDev)."""
         check(self.lib.irm_optimize_batch_dev(self._h, ctypes.byref(batch_dev), ctypes.c_void_p(stream)))

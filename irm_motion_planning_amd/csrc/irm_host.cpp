@@ -244,7 +244,8 @@ struct irm_ctx {
     KParams kp{};
     // device
     float *d_K = nullptr, *d_dK = nullptr, *d_Kt = nullptr, *d_dKt = nullptr, *d_F1 = nullptr, *d_F2 = nullptr,
-          *d_F1p = nullptr, *d_F2p = nullptr, *d_Fbot = nullptr, *d_Vr = nullptr, *d_H = nullptr, *d_u = nullptr, *d_w = nullptr;
+          *d_F1p = nullptr, *d_F2p = nullptr, *d_Fbot = nullptr, *d_Vr = nullptr, *d_H = nullptr, *d_u = nullptr, *d_w = nullptr,
+          *d_VTp = nullptr, *d_VNp = nullptr, *d_HV = nullptr;
     // host-API staging
     void* d_io = nullptr;
     size_t io_bytes = 0;
@@ -255,6 +256,8 @@ struct irm_ctx {
     int max_series = 0;
     unsigned long long* d_prof = nullptr;  // IRM_PHASE_PROFILE builds only
     int prof_blocks = 0, prof_cap = 0;
+    float* d_trace = nullptr;  // BLS line-search log of problem 0 (irm_debug_bls_trace)
+    int trace_cap = 0;
 };
 
 namespace {
@@ -308,6 +311,11 @@ int choose_shape(const irm_ctx* c, int B, bool optimizer, KParams& kp, int* lds_
         kp.BT = tb * kp.NW;
         if (pad_ok && 2 * ((B + tb - 1) / tb) <= c->num_cus && kp.BT < 512) kp.BT = 512;
         kp.nsplit = irm::stage1_splits(kp.NK);
+        // the lean GD kernel (k_gd_single) runs one stage-1 unit per wave: small workgroups of a GD
+        // single-loop launch get idle waves up to that count (e.g. one N = 128 trajectory per
+        // workgroup: 2 → 4 waves), so that the lean kernel — and its fp32-α rounding — serves them
+        if (optimizer && kp.optimizer == IRM_OPT_GD && kp.max_outer <= 1 && !kp.record_series)
+            kp.BT = std::max(kp.BT, std::min(512, 64 * (kp.RP / 16) * kp.nsplit));
         if (optimizer) {
             kp.regops = irm::regops_fit(kp) ? 1 : 0;
             irm::Plan a = irm::plan_lds(kp, true, true);
@@ -573,6 +581,29 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
         }
     rc |= upload(&c->d_Fbot, fb);
     rc |= upload(&c->d_Vr, vr);
+    {  // the lean kernel's α-space terms: V_Rᵀ (RP × NK) and V_R (NK × RP), k-permuted fragments,
+       // and G's endpoint velocity columns hv_e = V_R·F[N+e]ᵀ (e ∈ {0, N−1}), NK each
+        A.assign((size_t)RP * NK, 0.0);
+        for (int n = 0; n < N; ++n)
+            for (int r = 0; r < RP; ++r) A[(size_t)r * NK + n] = Vd[(size_t)n * RP + r];
+        fill_frag(frag, RP, NK, A, true);
+        rc |= upload(&c->d_VTp, frag);
+        A.assign((size_t)NK * RP, 0.0);
+        for (int n = 0; n < N; ++n)
+            for (int r = 0; r < RP; ++r) A[(size_t)n * RP + r] = Vd[(size_t)n * RP + r];
+        fill_frag(frag, NK, RP, A, true);
+        rc |= upload(&c->d_VNp, frag);
+        std::vector<float> hv((size_t)2 * NK, 0.f);
+        for (int e = 0; e < 2; ++e) {
+            const int me = N + (e ? N - 1 : 0);
+            for (int n = 0; n < N; ++n) {
+                double acc = 0.0;
+                for (int r = 0; r < RP; ++r) acc += Vd[(size_t)n * RP + r] * F[(size_t)me * RP + r];
+                hv[(size_t)e * NK + n] = (float)acc;
+            }
+        }
+        rc |= upload(&c->d_HV, hv);
+    }
     {  // h_e = F·F[N+e]ᵀ for the endpoint velocity rows e ∈ {0, N−1}, kernel row layout
         std::vector<float> h((size_t)2 * MP, 0.f);
         for (int e = 0; e < 2; ++e) {
@@ -632,6 +663,9 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
     kp.eps_v = p->eps_velocity;
     kp.lmax = p->lambda_max_cost;
     kp.lreg = p->lambda_reg;
+    // GD single loop's weight decay (1 − λ_reg·lr): Python floats, cast to fp32 where they meet α
+    // (optimizer_GD.py:81)
+    kp.gd_c0 = (float)(1.0 - decimal_double(p->lambda_reg) * decimal_double(p->gd_lr[0]));
     kp.bls_lr0 = p->bls_lr_start;
     kp.bls_a = p->bls_alpha;
     kp.bls_bp = p->bls_beta_plus;
@@ -726,6 +760,9 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
     kp.Fbot = c->d_Fbot;
     kp.Vr = c->d_Vr;
     kp.Hend = c->d_H;
+    kp.VTp = c->d_VTp;
+    kp.VNp = c->d_VNp;
+    kp.HV = c->d_HV;
     kp.uvec = c->d_u;
     kp.wvec = c->d_w;
     kp.lam_max = p->lambda_max_cost;
@@ -763,11 +800,12 @@ void irm_ctx_destroy(irm_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->p.device);
     float* bufs[] = {c->d_K, c->d_dK, c->d_Kt, c->d_dKt, c->d_F1,   c->d_F2, c->d_F1p, c->d_F2p,
-                     c->d_Fbot, c->d_Vr, c->d_H, c->d_u, c->d_w};
+                     c->d_Fbot, c->d_Vr, c->d_H, c->d_u, c->d_w, c->d_VTp, c->d_VNp, c->d_HV};
     for (float* b : bufs)
         if (b) (void)hipFree(b);
     if (c->d_io) (void)hipFree(c->d_io);
     if (c->d_prof) (void)hipFree(c->d_prof);
+    if (c->d_trace) (void)hipFree(c->d_trace);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -789,6 +827,29 @@ int irm_get_info(const irm_ctx* c, irm_info* out) {
 }
 
 int32_t irm_series_capacity(const irm_ctx* c) { return c ? c->max_series : 0; }
+
+int irm_debug_bls_trace_enable(irm_ctx* c, int32_t cap) {
+    if (!c || cap < 0) return fail(IRM_EINVAL, "irm_debug_bls_trace_enable: bad argument");
+    if (set_device(c)) return IRM_EDEVICE;
+    if (c->d_trace) (void)hipFree(c->d_trace);
+    c->d_trace = nullptr;
+    c->trace_cap = 0;
+    if (cap == 0) return IRM_OK;
+    HIP_TRY(hipMalloc(&c->d_trace, (size_t)cap * irm::kTraceW * sizeof(float)));
+    HIP_TRY(hipMemset(c->d_trace, 0, (size_t)cap * irm::kTraceW * sizeof(float)));
+    c->trace_cap = cap;
+    return IRM_OK;
+}
+
+int irm_debug_bls_trace(irm_ctx* c, float* out, int32_t cap) {
+    if (!c || !out || cap < 0) return fail(IRM_EINVAL, "irm_debug_bls_trace: bad argument");
+    if (!c->d_trace) return fail(IRM_EINVAL, "line-search log not enabled (irm_debug_bls_trace_enable)");
+    if (set_device(c)) return IRM_EDEVICE;
+    const int n = std::min(cap, c->trace_cap);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(out, c->d_trace, (size_t)n * irm::kTraceW * sizeof(float), hipMemcpyDeviceToHost));
+    return n;
+}
 
 int irm_debug_phase_profile(irm_ctx* c, uint64_t* out, int32_t max_blocks) {
     if (!c || !out) return fail(IRM_EINVAL, "null argument");
@@ -1024,6 +1085,8 @@ int irm_optimize_batch_dev(irm_ctx* c, const irm_batch_dev* a, void* stream) {
     kp.traj_out = a->traj_out;
     kp.stats = a->stats_out;
     kp.series = a->series_out;
+    kp.trace = c->d_trace;
+    kp.trace_cap = c->trace_cap;
     if (choose_shape(c, a->batch, true, kp, nullptr) <= 0) return fail(IRM_EINVAL, "no workgroup shape fits LDS");
 #ifdef IRM_PHASE_PROFILE
     {

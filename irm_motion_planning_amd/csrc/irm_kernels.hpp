@@ -43,7 +43,7 @@ struct KParams {
     int32_t lean_ok;  // k_gd_single may serve GD single-loop launches (IRM_GENERAL_KERNEL=1 clears it)
     int32_t lean_wpl; // diagnostics: IRM_LEAN_WPL=2 forces two waypoints per lane at N ≤ 128
     float llr, lci, lsg0, ljl0, eps_p, eps_v, lmax, lreg;
-    float bls_lr0, bls_a, bls_bp, bls_bm, vmax, pmax, pmin, pad1;
+    float bls_lr0, bls_a, bls_bp, bls_bm, vmax, pmax, pmin, gd_c0;  // gd_c0 = fp32(1 − λ_reg·lr₀) from doubles
     // derived fp32 constants (reference casts its Python doubles to fp32)
     float mean_pos, std_pos, std2, vmax2, thr_hi, thr_lo, thr_v, invN;
     float inv_std_pos, inv_vmax, inv_std2, inv_vmax2;  // reciprocals: x/c → x·(1/c) in the hot loops
@@ -67,6 +67,10 @@ struct KParams {
     const float* Fbot;    // F rows N..2N-1, row-major    (N × RP)
     const float* Vr;      // V_R, row-major               (N × RP)
     const float* Hend;    // F·F[NK]ᵀ, F·F[NK+N−1]ᵀ: operator columns of the endpoint velocity rows (2 × MP)
+    // V_R in the k-permuted fragment layouts of the lean kernel's fp32-α rounding terms
+    const float* VTp;     // V_Rᵀ (RP × NK): z = V_Rᵀ·e' (the rounding residual of α into waypoint space)
+    const float* VNp;     // V_R (NK × RP):  G = V_R·y'·J⁻¹ (the α-space gradient, per waypoint)
+    const float* HV;      // V_R·F[NK]ᵀ, V_R·F[NK+N−1]ᵀ: G's endpoint velocity columns (2 × NK)
     const float* uvec;    // K⁻¹(1-c)   (N)  initTrajectory basis
     const float* wvec;    // K⁻¹c       (N)
     // batch I/O
@@ -86,7 +90,12 @@ struct KParams {
     float* out1;   // grad: B×N×D
     uint8_t* out_ok;
     unsigned long long* prof;  // IRM_PHASE_PROFILE builds: per-block phase cycle counters
+    // diagnostics: BLS line-search log of problem 0 (irm_debug_bls_trace), kTraceW floats per trial
+    float* trace;
+    int32_t trace_cap;
 };
+
+constexpr int kTraceW = 10;  // outer, inner, trial, lr, new_loss, required_loss, accepted, loss, ‖g‖, alpha_norm
 
 constexpr int kProfPhases = 24;
 
@@ -142,7 +151,8 @@ struct Head {
 enum ColdWord : int {
     C_GDLR = 0,  // IRM_MAX_LR words
     C_LCI = 32, C_EPSP, C_EPSV, C_PMAX, C_PMIN, C_VMAX, C_BLR0, C_BA, C_BP, C_BM, C_MAXOUT, C_MAXBLS, C_MAXSER,
-    C_PTR = 46,     // 4 pointers × 2 words: series, Vr, Kt, dKt
+    C_TRCAP = 45,   // line-search log capacity (records)
+    C_PTR = 46,     // 5 pointers × 2 words: series, Vr, Kt, dKt, trace
     C_MINV = 56,    // (JᵀJ)⁻¹, D×D
     C_WAL = 120,    // D
     C_JINV = 128,   // J⁻¹, D×D
@@ -203,6 +213,41 @@ __host__ __device__ inline Plan plan_lds(const KParams& p, bool ops_lds, bool op
     return L;
 }
 
+
+// LDS of the lean GD kernel (k_gd_single) beyond the optimiser head + obstacles (`base`): the
+// endpoint operator columns hL (2·MP), G's endpoint columns hV (2·NK), the V_R fragments (when
+// staged: vlds), the rounding residual rows e' ([column][waypoint], stride NK + 8), its stage-1
+// partials zp ([split][column][r], stride RP + 8) and the gradient rows G ([column][waypoint]).
+struct LeanX {
+    int hl, hv, vt, vn, eb, zp, gb, total;
+};
+__host__ __device__ constexpr int lean_ld(int NK) { return NK + 8; }
+__host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, int nsplit, bool vlds) {
+    LeanX e{};
+    int off = base;
+    e.hl = off;
+    off += al4(2 * MP);
+    e.hv = off;
+    off += al4(2 * NK);
+    e.vt = e.vn = 0;
+    if (vlds) {
+        e.vt = off;
+        off += al4((int)frag_floats(RP, NK));
+        e.vn = off;
+        off += al4((int)frag_floats(NK, RP));
+    }
+    e.eb = off;
+    off += al4(16 * lean_ld(NK));
+    e.zp = off;
+    off += al4(nsplit * 16 * (RP + 8));
+    e.gb = off;
+    off += al4(16 * lean_ld(NK));
+    e.total = off;
+    return e;
+}
+// V_R fragments staged in LDS for the lean kernel: N ≤ 128 at D ≤ 3 (C7's two 256-thread
+// workgroups per CU and every N = 256 shape read them from L2 instead: LDS budget)
+__host__ __device__ constexpr bool lean_vlds(int NK, int D) { return NK <= 128 && D <= 3; }
 
 // Stage-1 split-K factor: units of 4 k-quads over the position half.
 __host__ __device__ constexpr int stage1_splits(int NK) { return (NK / 16 + 3) / 4; }

@@ -762,9 +762,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
         else if (i == C_MAXOUT) val = __int_as_float(P.max_outer);
         else if (i == C_MAXBLS) val = __int_as_float(P.max_bls);
         else if (i == C_MAXSER) val = __int_as_float(P.max_series);
-        else if (i >= C_PTR && i < C_PTR + 8) {
+        else if (i == C_TRCAP) val = __int_as_float(P.trace ? P.trace_cap : 0);
+        else if (i >= C_PTR && i < C_PTR + 10) {
             const int w = i - C_PTR;
-            const void* ptrs[4] = {P.series, P.Vr, P.Kt, P.dKt};
+            const void* ptrs[5] = {P.series, P.Vr, P.Kt, P.dKt, P.trace};
             const uint64_t a = reinterpret_cast<uint64_t>(ptrs[w >> 1]);
             val = __uint_as_float((w & 1) ? (uint32_t)(a >> 32) : (uint32_t)a);
         } else if (i >= C_MINV && i < C_MINV + D * D) val = P.Minv[i - C_MINV];
@@ -1234,6 +1235,21 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                 st.cost_evals++;
                 st.bls_trials++;
                 const float required = loss - cold[C_BA] * lr * anorm;
+                // line-search log of problem 0 (diagnostics; the reference's per-trial values,
+                // optimizer_BLS.py:139-149, 163-166)
+                if (b == 0 && n == 0 && st.bls_trials - 1 < cold_int(C_TRCAP)) {
+                    float* r = cold_ptr(4) + (size_t)(st.bls_trials - 1) * kTraceW;
+                    r[0] = (float)outer;
+                    r[1] = (float)inner;
+                    r[2] = (float)trial;
+                    r[3] = lr;
+                    r[4] = nl;
+                    r[5] = required;
+                    r[6] = (nl > required) ? 0.f : 1.f;
+                    r[7] = loss;
+                    r[8] = gnorm;
+                    r[9] = anorm;
+                }
                 bool inner_end = false, rejected_all = false;
                 float improve = 0.f;
                 if (nl > required) {
@@ -1337,19 +1353,36 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
 
 // ------------------------------------------- GD single loop, lean optimiser
 // optimizer_GD.py jit_optimize (max_outer_iteration == 1, dualOptimization false;
-// optimizer_GD.py:68-97): g = ∇L(α); α' = (1 − λ_reg·lr)·α − lr·g; accept iff
+// optimizer_GD.py:68-97): G = ∇L(α); α' = (1 − λ_reg·lr)·α − lr·G; accept iff
 // L − L(α') ≥ loop_loss_reduction, else stop keeping α; at most max_inner steps; then
-// α is materialised and constraintsFulfilled decides constraints_ok (k_optimize's
-// PH_RESYNC).  The same arithmetic as k_optimize's GD rounds (bit-identical results for
-// N ≤ 128, tests/test_gpu_parity.py::test_lean_gd_kernel_matches_general) without the
-// general state machine: every trajectory is either stepping or done, so a round needs no
-// phase logic, no direction / resync masks; one parity flag word per round (bit per wave
-// still stepping, bit 31 = dense stage 1) is OR-ed by the wave leaders and read by every
-// wave after the end barrier.  Shape-specialised, operators register-resident only.
+// constraintsFulfilled(α) decides constraints_ok.  Without the general state machine: every
+// trajectory is either stepping or done, so a round needs no phase logic, no direction / resync
+// masks; one parity flag word per round (bit per wave still stepping, bit 31 = dense stage 1) is
+// OR-ed by the wave leaders and read by every wave after the end barrier.  Shape-specialised,
+// F operators register-resident.
+//
+// α is carried in fp32 with the reference's rounding.  The reference iterates α (|α| ≈ 1e3, ulp
+// ≈ 6e-5, singular K) in fp32: α' = fl(fl(c·α) − fl(lr·G)) — and the rounding of c·α is biased
+// (c = 1 − 1.8e-7 moves α by 1.5–3 ulp per step), so its iterate drifts from the same iteration in
+// exact arithmetic by ~1e-2 in waypoint space over 200 steps, 10× its own ±1-ulp sensitivity
+// (tests/test_reference_bench.py).  Each lane therefore keeps its waypoint's α row
+// and applies exactly that update.  The gradient inputs are mixed by Jᵀ when written ([a'; b'] =
+// [a; b]·Jᵀ), so stage 1 gives y'' = Fᵀ[a; b]·Jᵀ and G = Lᵀ[a; b]·Jᵀ = V_R·y'' comes from a
+// stage-2 tile set (G's endpoint velocity columns through hV) with no mix; the waypoint state
+// [T; V] = L·α·J follows the exact part c·[T; V] − lr·(F·y'')·J as before, and the rounding
+// residual e = α' − (c·α − lr·G) (error-free transformations: fma residuals and TwoSum) enters
+// one round later through stage 1: z = V_Rᵀ·e', e' = −e/lr, is added to y'' on the way into stage
+// 2's F tiles, i.e. [T; V] += L·e·J (rank R: the discarded part is below σ_R / σ_0 ≈ 1e-6 of it).
+// Only J enters the per-lane mixes (D² scalars: at D = 7 three D×D matrices spilled SGPRs).  The
+// evaluation point of a round therefore lags the exact L·α·J by one residual (≤ 1e-4 in
+// waypoints, the size of the reference's own fp32 K@α noise); α itself is bit-for-bit the
+// reference's update of the G the kernel computes, and the epilogue returns it with
+// traj_out = K·α_out·J correctly rounded.
 // LDS is column-major here — X / dP as [column][row] (stride MP + 8), the stage-1 partials as
-// [split][column][r] (stride RP + 8) — with the k-permuted operator fragments (F1p / F2p,
-// frag_index_kp): a lane's four B values of a k-group are then one ds_read_b128 and an MFMA
-// result tile one ds_write_b128 per lane (strides ≡ 8 mod 16 keep both conflict-free).
+// [split][column][r] (stride RP + 8), e' and G as [column][waypoint] (stride NK + 8) — with the
+// k-permuted operator fragments (F1p / F2p / VTp / VNp, frag_index_kp): a lane's four B values of
+// a k-group are then one ds_read_b128 and an MFMA result tile one ds_write_b128 per lane (strides
+// ≡ 8 mod 16 keep both conflict-free).
 // WPL waypoints per lane (lane li of a trajectory owns waypoints li + j·NW/WPL): WPL = 2 lets
 // N = 256 trajectories run four to a 512-thread workgroup (C4) without exceeding 256 VGPRs.
 template <int WPL>
@@ -1412,6 +1445,31 @@ __device__ __forceinline__ void ered_store_wpl(const bool (&live)[WPL], const fl
     }
 }
 
+// A value the compiler may not fuse into a neighbouring operation (hipcc contracts a·b − c into
+// an fma even under `#pragma clang fp contract(off)` when the product comes from __fmul_rn).
+__device__ __forceinline__ float unfused(float x) {
+    asm("" : "+v"(x));
+    return x;
+}
+
+// One fp32 α element of the reference's GD / BLS update and its rounding residual:
+//   α' = fl(fl(c·α) − fl(lr·ĝ))                        (optimizer_GD.py:81, optimizer_BLS.py:139)
+//   e  = α' − (c·α − step·G)  exactly (to fp32 rounding of e itself), where c·[T; V] − step·F·y'
+//        is the waypoint-space update the kernel applies (ĝ = G for GD, G/‖G‖ for BLS).
+// Products and the subtraction are rounded separately (the reference's arithmetic, no fma); the
+// residuals come from fma (c·α − fl(c·α) is exact) and TwoSum.
+__device__ __forceinline__ float alpha_step(float al, float c, float lr, float gh, float step, float G, float& e) {
+    const float p1 = unfused(c * al), p2 = unfused(lr * gh);
+    const float an = unfused(p1 - p2);
+    const float ep1 = fmaf(c, al, -p1);                 // c·α − p1
+    const float bb = an - p1;                           // TwoSum(p1, −p2) = an + es
+    const float es = (p1 - (an - bb)) + (-p2 - bb);
+    const float p = unfused(step * G);
+    const float ep = fmaf(step, G, -p);                 // step·G − p
+    e = (((p - p2) - es) + ep) - ep1;                   // α' − (c·α − step·G)
+    return an;
+}
+
 // FULL: the launch has exactly MAXT threads, so the stage-2 tiles per wave are known exactly
 // (otherwise kS2T(MAXT) bounds them for smaller launches): C7's 256-thread variant then holds 4
 // tiles of operator fragments instead of 8 (32 VGPRs) and does not spill.
@@ -1425,6 +1483,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
     constexpr bool RV = MAXT > 256 || WPL > 1;  // velocity half of stage 1 register-resident too
     constexpr int NWL = S::NW / WPL;  // lanes per trajectory
     constexpr int WPTL = NWL / 64;    // waves per trajectory
+    constexpr bool VL = lean_vlds(S::NK, D);  // V_R fragments staged in LDS (else read from L2)
     static_assert(NWL % 64 == 0, "whole waves per trajectory");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const S sh(P);
@@ -1447,7 +1506,6 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
         nn[j] = li + j * NWL;
         vl[j] = tvalid && nn[j] < N;
     }
-    const bool yrow = tvalid && li < RP;
     const size_t b = (size_t)(tb0 + (tvalid ? t : 0));
     Prof prof;
     if (tid == 0) prof.init();
@@ -1455,15 +1513,22 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
     float* X = smem + H.X;
     float* dP = smem + H.dP;
     float* Ypart = smem + H.Ypart;
-    float* Ymix = smem + H.Ymix;
     float* red = smem + H.red;
     float* sg = smem + H.sg;
     unsigned* fw = reinterpret_cast<unsigned*>(smem + H.flags);
     float* obsL = smem + H.obs;
-
-    const int KQ1 = MP / 16, KQa = NK / 16, MT1 = RP / 16, KQ2 = RP / 16, MT2 = MP / 16;
     const int nsplit = sh.NSPLIT;
-    const int ldx = MP + 8, ldy = RP + 8;  // column strides of X / dP and of the stage-1 partials
+    const LeanX LX = lean_extra(plan_lds(P, false, true).total, MP, NK, RP, nsplit, VL);
+    float* hL = smem + LX.hl;  // endpoint columns of F·Fᵀ (2·MP), read per round when WPL > 1
+    float* hVL = smem + LX.hv; // G's endpoint columns (2·NK), read per round when WPL > 1
+    float* Eb = smem + LX.eb;  // e' rows [column][waypoint]
+    float* Zp = smem + LX.zp;  // stage-1 partials of V_Rᵀ·e'
+    float* Gb = smem + LX.gb;  // (V_R·y')[waypoint] rows [column][waypoint]
+    const float* VT = VL ? smem + LX.vt : P.VTp;
+    const float* VN = VL ? smem + LX.vn : P.VNp;
+
+    const int KQ1 = MP / 16, KQa = NK / 16, MT1 = RP / 16, KQ2 = RP / 16, MT2 = MP / 16, MTG = NK / 16;
+    const int ldx = MP + 8, ldy = RP + 8, lde = lean_ld(NK);  // column strides
     const int cl = lane & 15, r4 = 4 * (lane >> 4);  // MFMA column / first of 4 rows of this lane
     const bool has1 = wave < MT1 * nsplit;
     const int tile1 = wave % MT1, sp1 = wave / MT1;
@@ -1495,23 +1560,38 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
     // endpoint operator columns: in VGPRs for one waypoint per lane; with two (C4: 256 VGPRs) they
     // are read from an LDS copy each round instead, which keeps the variant free of scratch spills
     constexpr bool kHL = WPL > 1;
-    float* hL = smem + plan_lds(P, false, true).total;  // 2·MP floats (lean_lds)
-    float h0T[WPL], h1T[WPL], h0V[WPL], h1V[WPL];
+    float h0T[WPL], h1T[WPL], h0V[WPL], h1V[WPL], hv0[WPL], hv1[WPL];
 #pragma unroll
     for (int j = 0; j < WPL; ++j) {
         h0T[j] = (vl[j] && !kHL) ? P.Hend[nn[j]] : 0.f;
         h1T[j] = (vl[j] && !kHL) ? P.Hend[MP + nn[j]] : 0.f;
         h0V[j] = (vl[j] && !kHL) ? P.Hend[NK + nn[j]] : 0.f;
         h1V[j] = (vl[j] && !kHL) ? P.Hend[MP + NK + nn[j]] : 0.f;
+        hv0[j] = (vl[j] && !kHL) ? P.HV[nn[j]] : 0.f;
+        hv1[j] = (vl[j] && !kHL) ? P.HV[NK + nn[j]] : 0.f;
     }
-    if constexpr (kHL)
+    if constexpr (kHL) {
         for (int e = tid; e < 2 * MP; e += P.BT) hL[e] = P.Hend[e];
+        for (int e = tid; e < 2 * NK; e += P.BT) hVL[e] = P.HV[e];
+    }
+    if constexpr (VL) {
+        const int nv = (int)frag_floats(RP, NK) / 4;  // = frag_floats(NK, RP) / 4
+        const f32x4* gt = reinterpret_cast<const f32x4*>(P.VTp);
+        const f32x4* gn = reinterpret_cast<const f32x4*>(P.VNp);
+        f32x4* lt = reinterpret_cast<f32x4*>(smem + LX.vt);
+        f32x4* ln = reinterpret_cast<f32x4*>(smem + LX.vn);
+        for (int e = tid; e < nv; e += P.BT) {
+            lt[e] = gt[e];
+            ln[e] = gn[e];
+        }
+    }
+    for (int e = tid; e < 16 * lde; e += P.BT) Eb[e] = 0.f;  // no pending residual; rows ≥ N stay 0
     stage_obstacles(P, tb0, ntb, obsL);
     stage_alpha<D>(P, tb0, ntb, X, NK);
     if (tid < 2) fw[tid] = 0u;
     __syncthreads();
-    // α0 is not kept in registers: the epilogue restages it (stage_alpha is deterministic)
-    float q[WPL][D], v[WPL][D], aca[WPL][D], acb[WPL][D];
+    // the reference's α (fp32, this lane's waypoint rows) and T0 = (K·α0)·J, V0 = (dK·α0)·J
+    float q[WPL][D], v[WPL][D], al[WPL][D];
     float s[D], g[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) {
@@ -1523,15 +1603,16 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
 #pragma unroll
         for (int k = 0; k < D; ++k) {
             q[j][k] = v[j][k] = 0.f;
-            aca[j][k] = acb[j][k] = 0.f;
+            al[j][k] = vl[j] ? X[nn[j] * kLd + t * D + k] : 0.f;
         }
-        if (vl[j]) eval_exact<D>(P, X + t * D, nn[j], q[j], v[j]);  // T0 = (K·α0)·J, V0 = (dK·α0)·J
+        if (vl[j]) eval_exact<D>(P, X + t * D, nn[j], q[j], v[j]);
     }
     __syncthreads();
     for (int e = tid; e < MP * kLd; e += P.BT) X[e] = 0.f;
     const float* obs = obsL + (P.obs_stride ? t * obs_pitch(P.O) : 0);
     const float lsg = P.lsg0, ljl = P.ljl0, lr = P.gd_lr[0];
-    const float cfac = 1.f - P.lreg * lr, step = lr;
+    const float cfac = P.gd_c0, step = lr;
+    const float nilr = -1.f / lr;  // e' = −e/lr: the update then adds −lr·(F·V_Rᵀe')·J = L·e·J
 
     // evaluation of (q2, v2) with this trajectory's waves: wave partials + endpoint rows
     auto evaluate = [&](const float (&q2)[WPL][D], const float (&v2)[WPL][D], bool ext, WP<D> (&w)[WPL]) {
@@ -1602,7 +1683,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
         f.va = va;
         return f;
     };
-    // gradient inputs at (q2, v2), mixed by JᵀJ, into X; returns "b' non-zero away from the endpoints"
+    // gradient inputs at (q2, v2), mixed by Jᵀ, into X; returns "b' non-zero away from the endpoints"
     auto grad_inputs = [&](const WP<D> (&w)[WPL], const float (&q2)[WPL][D], const float (&v2)[WPL][D], int cidx) {
         bool bfar = false;
 #pragma unroll
@@ -1617,8 +1698,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
                     float ma = 0.f, mb = 0.f;
 #pragma unroll
                     for (int d = 0; d < D; ++d) {
-                        ma += a[d] * P.JtJ[d * D + k];
-                        mb += bb[d] * P.JtJ[d * D + k];
+                        ma += a[d] * P.J[k * D + d];
+                        mb += bb[d] * P.J[k * D + d];
                     }
                     X[(t * D + k) * ldx + n] = ma;
                     X[(t * D + k) * ldx + NK + n] = mb;
@@ -1681,6 +1762,26 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
         }
         *reinterpret_cast<f32x4*>(Ypart + (sp1 * 16 + cl) * ldy + tile1 * 16 + r4) = acc0 + acc1;
     };
+    // z = V_Rᵀ·e' (the last accepted step's rounding residual), MT1 × nsplit units over the waves
+    // from the top down (C3: waves 4-7, idle in the Fᵀ stage), operator from LDS / L2
+    auto stage1z = [&]() {
+        const float* el = Eb + cl * lde + r4;
+        for (int u = nwaves - 1 - wave; u < MT1 * nsplit; u += nwaves) {
+            const int tile = u % MT1, sp = u / MT1;
+            const int k0 = (KQa * sp) / nsplit, k1 = (KQa * (sp + 1)) / nsplit;
+            const f32x4* ap = reinterpret_cast<const f32x4*>(VT) + (size_t)tile * KQa * 64 + lane;
+            f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+            for (int kq = k0; kq < k1; ++kq) {
+                const f32x4 a = ap[(size_t)kq * 64];
+                const f32x4 bb = *reinterpret_cast<const f32x4*>(el + kq * 16);
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], bb[0], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], bb[1], acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], bb[2], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], bb[3], acc1, 0, 0, 0);
+            }
+            *reinterpret_cast<f32x4*>(Zp + (sp * 16 + cl) * ldy + tile * 16 + r4) = acc0 + acc1;
+        }
+    };
 
     // round 0 (optimizer_GD.py:93: the loss at α0) and the first gradient inputs
     irm_stats st{};
@@ -1702,43 +1803,41 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
     IRM_STAMP(14);
     // ---------------------------------------------------------- GD rounds
     int inner = 0;
-    float cprod = 1.f;
     for (int par = 0;; par ^= 1) {
         const unsigned fl = fw[par];
         if ((fl & 0x7FFFFFFFu) == 0u) break;  // every trajectory of the block is done
         const bool dense = (fl >> 31) != 0u;
         if (tid == 0) fw[par ^ 1] = 0u;
-        // this lane's gradient-input rows (α recovery) and the endpoint velocity rows
-        float e0[D], e1[D], xa[WPL][D], xb[WPL][D];
+        // the endpoint velocity rows of this trajectory's gradient inputs (their operator columns)
+        float e0[D], e1[D];
 #pragma unroll
         for (int k = 0; k < D; ++k) {
             const float* xc = X + (t * D + k) * ldx;
             e0[k] = xc[NK];
             e1[k] = xc[NK + N - 1];
-#pragma unroll
-            for (int j = 0; j < WPL; ++j) {
-                const int nr = vl[j] ? nn[j] : 0;
-                xa[j][k] = xc[nr];
-                xb[j][k] = xc[NK + nr];
-            }
         }
         IRM_STAMP(0);
         IRM_COUNT(13, dense);
         stage1(dense);
+        stage1z();
         IRM_STAMP(1);
         __syncthreads();
         IRM_STAMP(2);
-        {  // stage 2: dP = F·Σ_s Ypart[s]
+        {  // stage 2: dP = F·(Σ_s Ypart[s] + Σ_s Zp[s]), Gb = V_R·Σ_s Ypart[s]
             f32x4 acc[S2T];
 #pragma unroll
             for (int j = 0; j < S2T; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-            f32x4 bv[2];
+            f32x4 by[2], bt[2];
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-                bv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                by[i] = bt[i] = f32x4{0.f, 0.f, 0.f, 0.f};
                 if (i < KQ2) {
-                    for (int sp = 0; sp < nsplit; ++sp)
-                        bv[i] += *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + cl) * ldy + i * 16 + r4);
+                    f32x4 bz = {0.f, 0.f, 0.f, 0.f};
+                    for (int sp = 0; sp < nsplit; ++sp) {
+                        by[i] += *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + cl) * ldy + i * 16 + r4);
+                        bz += *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + i * 16 + r4);
+                    }
+                    bt[i] = by[i] + bz;
                 }
             }
 #pragma unroll
@@ -1747,10 +1846,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
 #pragma unroll
                     for (int j = 0; j < S2T; ++j) {
                         if (wave + j * nwaves < MT2) {
-                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][0], bv[i][0], acc[j], 0, 0, 0);
-                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][1], bv[i][1], acc[j], 0, 0, 0);
-                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][2], bv[i][2], acc[j], 0, 0, 0);
-                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][3], bv[i][3], acc[j], 0, 0, 0);
+                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][0], bt[i][0], acc[j], 0, 0, 0);
+                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][1], bt[i][1], acc[j], 0, 0, 0);
+                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][2], bt[i][2], acc[j], 0, 0, 0);
+                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][3], bt[i][3], acc[j], 0, 0, 0);
                         }
                     }
                 }
@@ -1759,6 +1858,22 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
             for (int j = 0; j < S2T; ++j)
                 if (wave + j * nwaves < MT2)
                     *reinterpret_cast<f32x4*>(dP + cl * ldx + (wave + j * nwaves) * 16 + r4) = acc[j];
+            // G tiles (waypoint rows of V_R·y'), from the top wave down
+            for (int u = nwaves - 1 - wave; u < MTG; u += nwaves) {
+                const f32x4* ap = reinterpret_cast<const f32x4*>(VN) + (size_t)u * KQ2 * 64 + lane;
+                f32x4 ag = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    if (i < KQ2) {
+                        const f32x4 a = ap[(size_t)i * 64];
+                        ag = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], by[i][0], ag, 0, 0, 0);
+                        ag = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], by[i][1], ag, 0, 0, 0);
+                        ag = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], by[i][2], ag, 0, 0, 0);
+                        ag = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], by[i][3], ag, 0, 0, 0);
+                    }
+                }
+                *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4) = ag;
+            }
         }
         IRM_STAMP(3);
         __syncthreads();
@@ -1768,21 +1883,32 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
         if (!done) {  // wave-uniform
 #pragma unroll
             for (int j = 0; j < WPL; ++j) {
+                float ut[D], uv[D];
 #pragma unroll
                 for (int k = 0; k < D; ++k) {
-                    float ut = dP[(t * D + k) * ldx + nn[j]], uv = dP[(t * D + k) * ldx + NK + nn[j]];
+                    ut[k] = dP[(t * D + k) * ldx + nn[j]];
+                    uv[k] = dP[(t * D + k) * ldx + NK + nn[j]];
                     // endpoint velocity rows enter through their operator columns in every round
                     // (stage 1's operator has zero columns there: a dense round adds exact zeros)
                     if constexpr (kHL) {
                         const int r = vl[j] ? nn[j] : 0;
-                        ut = fmaf(hL[r], e0[k], fmaf(hL[MP + r], e1[k], ut));
-                        uv = fmaf(hL[NK + r], e0[k], fmaf(hL[MP + NK + r], e1[k], uv));
+                        ut[k] = fmaf(hL[r], e0[k], fmaf(hL[MP + r], e1[k], ut[k]));
+                        uv[k] = fmaf(hL[NK + r], e0[k], fmaf(hL[MP + NK + r], e1[k], uv[k]));
                     } else {
-                        ut = fmaf(h0T[j], e0[k], fmaf(h1T[j], e1[k], ut));
-                        uv = fmaf(h0V[j], e0[k], fmaf(h1V[j], e1[k], uv));
+                        ut[k] = fmaf(h0T[j], e0[k], fmaf(h1T[j], e1[k], ut[k]));
+                        uv[k] = fmaf(h0V[j], e0[k], fmaf(h1V[j], e1[k], uv[k]));
                     }
-                    q2[j][k] = cfac * q[j][k] - step * ut;
-                    v2[j][k] = cfac * v[j][k] - step * uv;
+                }
+#pragma unroll
+                for (int k = 0; k < D; ++k) {  // Δ[T; V] = (F·y'')·J
+                    float dt = 0.f, dv = 0.f;
+#pragma unroll
+                    for (int l = 0; l < D; ++l) {
+                        dt = fmaf(ut[l], P.J[l * D + k], dt);
+                        dv = fmaf(uv[l], P.J[l * D + k], dv);
+                    }
+                    q2[j][k] = cfac * q[j][k] - step * dt;
+                    v2[j][k] = cfac * v[j][k] - step * dv;
                 }
             }
             IRM_STAMP(5);
@@ -1805,18 +1931,22 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
             if (loss - f.nl < P.llr) {
                 done = true;  // minimized: the step is discarded (optimizer_GD.py:87-90)
             } else {
+                // accepted: α' = fl(fl(c·α) − fl(lr·G)) (optimizer_GD.py:81) and its residual e' for
+                // the next round's stage 1
 #pragma unroll
                 for (int j = 0; j < WPL; ++j) {
+                    const int r = vl[j] ? nn[j] : 0;
+                    const float v0 = kHL ? hVL[r] : hv0[j], v1 = kHL ? hVL[NK + r] : hv1[j];
 #pragma unroll
                     for (int k = 0; k < D; ++k) {
+                        const float G = fmaf(v0, e0[k], fmaf(v1, e1[k], Gb[(t * D + k) * lde + r]));
+                        float er;
+                        al[j][k] = alpha_step(al[j][k], cfac, lr, G, step, G, er);
                         q[j][k] = q2[j][k];
                         v[j][k] = v2[j][k];
-                        const float ra = vl[j] ? xa[j][k] : 0.f, rb = vl[j] ? xb[j][k] : 0.f;
-                        aca[j][k] = cfac * aca[j][k] + step * ra;  // α recovery: Σ steps·[a'; b']
-                        acb[j][k] = cfac * acb[j][k] + step * rb;
+                        if (vl[j]) Eb[(t * D + k) * lde + nn[j]] = nilr * er;
                     }
                 }
-                cprod *= cfac;
                 loss = f.nl;
                 inner++;
                 st.inner_iterations++;
@@ -1832,68 +1962,14 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
     }
 
     // ---------------------------------------------------------- epilogue
-    // α = cprod·α0 − V_R·(Fᵀ·acc)·J⁻¹ in fp32 (k_optimize's PH_RESYNC), T = eval_exact(α),
-    // constraintsFulfilled(α) (trajectory.py:129-137, robot.py:90-113).
+    // T = eval_exact(α) (correctly rounded K·α·J), constraintsFulfilled(α) (trajectory.py:129-137,
+    // robot.py:90-113) on it.  Every wave has left the loop after its last barrier: X is free.
     st.final_loss = loss;
-    float ab[WPL][D];
-#pragma unroll
-    for (int j = 0; j < WPL; ++j)
-#pragma unroll
-        for (int k = 0; k < D; ++k) ab[j][k] = 0.f;
 #pragma unroll
     for (int j = 0; j < WPL; ++j) {
         if (vl[j]) {
 #pragma unroll
-            for (int k = 0; k < D; ++k) {
-                X[(t * D + k) * ldx + nn[j]] = aca[j][k];
-                X[(t * D + k) * ldx + NK + nn[j]] = acb[j][k];
-            }
-        }
-    }
-    __syncthreads();
-    stage1(true);
-    stage_alpha<D>(P, tb0, ntb, dP, NK);  // α0 again, row-major into the (free) Δ buffer
-    __syncthreads();
-    if (yrow) {
-        const float fb0 = P.Fbot[li], fb1 = P.Fbot[(size_t)(N - 1) * RP + li];
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            // endpoint velocity rows through F's endpoint rows (stage 1's operator omits them)
-            const float* xc = X + (t * D + d) * ldx;
-            float y = fmaf(fb0, xc[NK], fb1 * xc[NK + N - 1]);
-            for (int sp = 0; sp < nsplit; ++sp) y += Ypart[(sp * 16 + t * D + d) * ldy + li];
-            Ymix[li * kLd + t * D + d] = y;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < WPL; ++j) {
-        if (vl[j]) {
-            const int n = nn[j];
-            float z[D];
-#pragma unroll
-            for (int l = 0; l < D; ++l) z[l] = 0.f;
-            const float* vr = P.Vr + (size_t)n * RP;
-            for (int r = 0; r < RP; ++r) {
-                const float vv = vr[r];
-#pragma unroll
-                for (int l = 0; l < D; ++l) z[l] += vv * Ymix[r * kLd + t * D + l];
-            }
-#pragma unroll
-            for (int k = 0; k < D; ++k) {
-                float acc = 0.f;
-#pragma unroll
-                for (int l = 0; l < D; ++l) acc += z[l] * P.Jinv[l * D + k];
-                ab[j][k] = cprod * dP[n * kLd + t * D + k] - acc;
-            }
-        }
-    }
-    __syncthreads();  // X is rewritten below
-#pragma unroll
-    for (int j = 0; j < WPL; ++j) {
-        if (vl[j]) {
-#pragma unroll
-            for (int k = 0; k < D; ++k) X[nn[j] * kLd + t * D + k] = ab[j][k];
+            for (int k = 0; k < D; ++k) X[nn[j] * kLd + t * D + k] = al[j][k];
         }
     }
     __syncthreads();
@@ -1917,7 +1993,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
 #pragma unroll
                 for (int k = 0; k < D; ++k) {
                     if (P.traj_out) P.traj_out[(b * N + nn[j]) * D + k] = q[j][k];
-                    if (P.alpha_out) P.alpha_out[(b * N + nn[j]) * D + k] = ab[j][k];
+                    if (P.alpha_out) P.alpha_out[(b * N + nn[j]) * D + k] = al[j][k];
                 }
             }
         }
@@ -2055,7 +2131,8 @@ struct type_tag {
 inline size_t lean_lds(const KParams& p) {
     KParams q = p;
     q.regops = 1;
-    return (size_t)(plan_lds(q, false, true).total + 2 * p.MP) * 4;  // + the endpoint columns (hL)
+    const int D = p.D;
+    return (size_t)lean_extra(plan_lds(q, false, true).total, p.MP, p.NK, p.RP, p.nsplit, lean_vlds(p.NK, D)).total * 4;
 }
 
 // k_optimize<Shape> with the MAXT / operator-placement / optimiser variants (one shape per
@@ -2075,14 +2152,14 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s) {
                 KParams q = p;
                 q.BT = p.BT / 2;
                 q.NW = p.NW / 2;
-                if (p.lean_wpl == 2 && q.lean_ok && q.optimizer == IRM_OPT_GD && q.max_outer == 1 &&
+                if (p.lean_wpl == 2 && q.lean_ok && q.optimizer == IRM_OPT_GD && q.max_outer <= 1 &&
                     !q.record_series && (q.RP / 16) * q.nsplit <= q.BT / 64 && q.NK / 16 <= 8 * q.nsplit)
                     return launch_lds(k_gd_single<Sh, 256, 2>, grid, q.BT, lean_lds(q), s, q);
             }
         }
         if constexpr (!Sh::kVariants && TT <= 512) {  // GD single loop: the lean kernel
             // (operators register-resident: one stage-1 unit per wave, enough waves for the units)
-            if (p.lean_ok && p.optimizer == IRM_OPT_GD && p.max_outer == 1 && !p.record_series &&
+            if (p.lean_ok && p.optimizer == IRM_OPT_GD && p.max_outer <= 1 && !p.record_series &&
                 (p.RP / 16) * p.nsplit <= p.BT / 64 && p.NK / 16 <= 4 * p.nsplit)
                 return p.BT == TT ? launch_lds(k_gd_single<Sh, TT, 1, true>, grid, p.BT, lean_lds(p), s, p)
                                   : launch_lds(k_gd_single<Sh, TT, 1>, grid, p.BT, lean_lds(p), s, p);
@@ -2093,7 +2170,7 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s) {
                 KParams q = p;
                 q.BT = p.BT / 2;
                 q.NW = p.NW / 2;
-                if (q.lean_ok && q.optimizer == IRM_OPT_GD && q.max_outer == 1 && !q.record_series &&
+                if (q.lean_ok && q.optimizer == IRM_OPT_GD && q.max_outer <= 1 && !q.record_series &&
                     (q.RP / 16) * q.nsplit <= q.BT / 64 && q.NK / 16 <= 4 * q.nsplit)
                     return launch_lds(k_gd_single<Sh, 512, 2>, grid, q.BT, lean_lds(q), s, q);
             }

@@ -311,27 +311,43 @@ def _ref64_band(r, a0, obs, s, g, iters, n_ens=2):
     return T64, l64, n, spread, lspread
 
 
-# With λmax > 0 a step whose argmax waypoint differs between fp32 and fp64 (a near-tie of two
-# waypoints' obstacle costs) moves the trajectory by ≈ lr·λmax·|∇cost|·|K| — measured up to
-# 4e-2 after 200 steps (C4 problem 0) while the final loss still agrees to 2e-4.
-ARGMAX_SLACK = 5e-2
+# Floor of the HIP-vs-oracle band after many GD steps.  Both iterate α in fp32 with the reference's
+# rounding, but their gradients differ in the last bits (rank-32 fp32 MFMA vs fp64-accumulated
+# contractions), which flips an occasional α rounding; the iteration amplifies such per-step noise
+# more than a single ±1 ulp on α0 (the spread).  The reference itself moves by 2.5e-3 - 1.9e-2 (C3)
+# and 7.8e-3 - 1.4e-1 (C4) after 200 steps between its fp32 BLAS matmuls and correctly rounded ones
+# (tests/golden/ref_bench_c{3,4}{,_xm}.npz); measured HIP vs oracle: ≤ 4e-3 at N = 128, ≤ 3.6e-3
+# at N = 256 where the ±1-ulp spread is ≥ 7e-4.
+ORACLE_FLOOR = 5e-3
 
 
-def _bench_vs_ref(cfg, B, n_check, iters=200, lmax=None, slack=1e-3):
-    """Bench mode (exactly `iters` GD steps per problem) against the reference algorithm in
-    exact (fp64) arithmetic, from the same α0 (the device's initTrajectory).
+def _oracle_band(o, a0, obs, s, g, n_ens=2):
+    """The C oracle's run (the reference's fp32 α iteration, correctly rounded contractions) and its
+    sensitivity: the largest waypoint / loss change when α0 moves by ±1 ulp."""
+    al, st = o.optimize(a0, obs, s, g)
+    T = o.evaluate(al)
+    spread = lspread = 0.0
+    for seed in range(n_ens):
+        sgn = np.random.default_rng(100 + seed).choice([-1.0, 1.0], a0.shape).astype(np.float32)
+        ap = np.nextafter(a0, a0 + sgn * np.float32(np.inf)).astype(np.float32)
+        ae, se = o.optimize(ap, obs, s, g)
+        spread = max(spread, float(np.abs(o.evaluate(ae) - T).max()))
+        lspread = max(lspread, abs(se["final_loss"] - st["final_loss"]))
+    return T, st, spread, lspread
 
-    Per problem: final loss within 1e-3 (relative) and
-      |traj − exact| ≤ 3·spread + 2·round + slack, where
-      spread — the exact iteration's own change under ±1 ulp on α0 (the max-cost term sends
-               its gradient to the argmax waypoint only, so near-ties separate nearby runs);
-      round  — |K·fp32(α)·J − K·α·J| of the exact α: returning α in fp32 (|α| ≈ 1e3, singular
-               K) moves the trajectory it represents by this much (traj_out is K·α_out·J).
-    (The reference's own fp32 α-space iteration drifts from the exact one by up to ~0.2 here —
-    test_oracle_golden.py::test_fp32_alpha_drift.)"""
+
+def _bench_vs_ref(cfg, B, n_check, iters=200, lmax=None):
+    """Bench mode (exactly `iters` GD steps per problem, k_gd_single) against the CPU oracle — the
+    reference's fp32 α iteration with its rounding, pinned to the reference's own output at C3 / C4
+    by tests/test_reference_bench.py — from the same α0 (the device's initTrajectory).
+
+    Per problem: |traj − oracle| ≤ max(2·spread, ORACLE_FLOOR), spread = the oracle's own change
+    under ±1 ulp on α0; final loss within 1e-3 relative + 3·(its ±1-ulp loss change).  (The same iteration in exact arithmetic,
+    oracle/ref64.py, ends 1-4e-2 away at C3: test_oracle_golden.py::test_fp32_alpha_drift.)"""
     import bench
     from irm_motion_planning_amd.context import Context
     from irm_motion_planning_amd.params import params_from_args
+    from oracle.oracle import Oracle
     args = bench.make_args(cfg, False, iters)
     if lmax is not None:
         args.lambda_max_cost = lmax
@@ -340,32 +356,31 @@ def _bench_vs_ref(cfg, B, n_check, iters=200, lmax=None, slack=1e-3):
     c = Context(params_from_args(args))
     alpha, traj, st = c.optimize(s, g, obs)
     assert np.all(st["grad_evals"] == iters) and np.all(np.isfinite(traj))
-    _, r = _ref64(args)
+    o = Oracle(params_from_args(args))
     for b in np.linspace(0, B - 1, n_check).astype(int):
         a0 = c.init_alpha(s[b], g[b])
-        T64, l64, n, spread, lspread = _ref64_band(r, a0, obs, s[b], g[b], iters)
-        a64, _, _ = r.gd_single(a0, obs, s[b], g[b], iters)
-        rnd = float(np.abs(r.traj_vel(a64.astype(np.float32))[0] - T64).max())
-        err = float(np.abs(traj[b] - T64).max())
-        print(f"{cfg}[{b}] lmax={args.lambda_max_cost} {iters} steps: |traj - exact| {err:.2e}, "
-              f"spread {spread:.2e}, round {rnd:.2e}, loss {float(st['final_loss'][b]):.6f} vs {l64:.6f}")
-        assert n == iters
-        assert err <= 3 * spread + 2 * rnd + slack, (b, err, spread, rnd)
-        assert abs(float(st["final_loss"][b]) - l64) <= 1e-3 * abs(l64) + 3 * lspread
+        T, so, spread, lspread = _oracle_band(o, a0, obs, s[b], g[b])
+        err = float(np.abs(traj[b] - T).max())
+        band = max(2.0 * spread, ORACLE_FLOOR)
+        print(f"{cfg}[{b}] lmax={args.lambda_max_cost} {iters} steps: |traj - oracle| {err:.2e} (spread {spread:.2e}), "
+              f"loss {float(st['final_loss'][b]):.6f} vs {so['final_loss']:.6f}")
+        assert so["grad_evals"] == iters
+        assert err <= band, (b, err, spread)
+        assert abs(float(st["final_loss"][b]) - so["final_loss"]) <= 1e-3 * abs(so["final_loss"]) + 3 * lspread
     return c, alpha, traj, st
 
 
 @pytest.mark.parametrize("cfg,B", [("c3", 256), ("c4", 32), ("c5", 16), ("c7", 32)])
-def test_bench_smooth_objective_tracks_exact_iteration(cfg, B):
-    """λmax = 0 (mean obstacle cost only): 200 steps within 2e-3 (+ sensitivity) of exact."""
+def test_bench_smooth_objective_tracks_oracle(cfg, B):
+    """λmax = 0 (mean obstacle cost only): 200 steps inside the oracle band."""
     _bench_vs_ref(cfg, B, 4, lmax=0.0)
 
 
 def test_bench_c3_full_size_properties():
     """BASELINE configs[2] at full size (1024 × N=128): every problem runs exactly 200 GD
     iterations, K@α_out@J reproduces traj_out bit for bit, results are deterministic, and
-    a spread of problems matches the exact-arithmetic reference."""
-    c, alpha, traj, st = _bench_vs_ref("c3", 1024, 8, slack=ARGMAX_SLACK)
+    a spread of problems matches the oracle (the reference's fp32 α iteration)."""
+    c, alpha, traj, st = _bench_vs_ref("c3", 1024, 8)
     import bench
     np.testing.assert_array_equal(c.evaluate(alpha[::97]), traj[::97])
     s, g, obs = bench.make_problem("c3", 1, 0)
@@ -374,16 +389,16 @@ def test_bench_c3_full_size_properties():
 
 
 def test_bench_c4_random_obstacles():
-    _bench_vs_ref("c4", 64, 4, slack=ARGMAX_SLACK)
+    _bench_vs_ref("c4", 64, 4)
 
 
 def test_bench_c5_seven_dof():
-    _bench_vs_ref("c5", 32, 3, slack=ARGMAX_SLACK)
+    _bench_vs_ref("c5", 32, 3)
 
 
 def test_bench_c7_seven_dof_n128():
     """north_star's target shape (7-DoF, 128 waypoints; FixShape<7, 128>, lean kernel)."""
-    _bench_vs_ref("c7", 64, 4, slack=ARGMAX_SLACK)
+    _bench_vs_ref("c7", 64, 4)
 
 
 @pytest.mark.parametrize("cfg", ["c3", "c4", "c7"])
@@ -438,8 +453,7 @@ def test_per_problem_obstacles_and_edge_counts():
     """obstacle_stride > 0: each problem its own obstacle set; also O = 0 and O = 64."""
     args = ("--optimizer-name", "gd", "--max-outer-iteration", 1, "--max-inner-iteration", 30)
     c = ctx(*args)
-    from conftest import ref_args
-    o, r = _ref64(ref_args(*args))
+    o = oracle_for(*args)
     rng = np.random.default_rng(5)
     B = 5
     s = rng.uniform(-0.5, 0.5, (B, 3)).astype(np.float32)
@@ -449,13 +463,11 @@ def test_per_problem_obstacles_and_edge_counts():
         _, traj, st = c.optimize(s, g, obs, obstacle_stride=2 * O)  # stride in floats (irm.h)
         for b in range(B):
             a0 = c.init_alpha(s[b], g[b])
-            T64, _, n, spread, _ = _ref64_band(r, a0, obs[b], s[b], g[b], 30)
-            a64, _, _ = r.gd_single(a0, obs[b], s[b], g[b], 30)
-            rnd = float(np.abs(r.traj_vel(a64.astype(np.float32))[0] - T64).max())
-            err = float(np.abs(traj[b] - T64).max())
-            assert err <= 3 * spread + 2 * rnd + 1e-3, (O, b, err, spread, rnd)  # see _bench_vs_ref
+            T, so, spread, _ = _oracle_band(o, a0, obs[b], s[b], g[b])
+            err = float(np.abs(traj[b] - T).max())
+            assert err <= max(2.0 * spread, 1e-3), (O, b, err, spread)  # see _bench_vs_ref
             if spread < 1e-4:  # the loop-exit step is only defined where the iteration is stable
-                assert int(st["grad_evals"][b]) == min(n + 1, 30)
+                assert int(st["grad_evals"][b]) == so["grad_evals"]
 
 
 def test_device_pointer_entry_point():
@@ -530,20 +542,17 @@ def test_object_api(g_e2e):
                                         (256, "bench", 3, 2), (256, "faithful", 3, 2), (256, "bench", 7, 2),
                                         (256, "bench", 3, 4), (256, "faithful", 3, 4),
                                         (128, "bench", 7, 0), (128, "faithful", 7, 0)])
-def test_lean_gd_kernel_matches_general(N, mode, D, tb):
+def test_lean_gd_kernel_matches_oracle(N, mode, D, tb):
     """k_gd_single (GD single loop, shape-specialised; at N = 256 with four trajectories per
-    workgroup the two-waypoints-per-lane variant) vs the general k_optimize
-    (IRM_GENERAL_KERNEL=1) on the same problems.  Same algorithm and state, but the lean kernel
-    feeds the MFMAs k-permuted operators (frag_index_kp), so the 4-term partial sums inside each
-    MFMA group differently and the two kernels are two fp32 roundings of the same iteration
-    (tools/pad_check.py: never bit-equal once the lean kernel runs).  B = 48 problems occupy
-    48 workgroups at tb = 0, so the launch is padded to 512 threads (IRM_PAD_WAVES), which is
-    what makes the lean kernel eligible at one trajectory per workgroup.  Bound: waypoints
-    within 5e-3 (1e-2 at D = 7; measured ≤ 3.7e-3 / 4.6e-3 at N = 128 after 60 steps; each kernel separately tracks the
-    exact-arithmetic iteration, test_bench_*), final loss within 2e-4 relative.  In faithful mode
-    a trajectory whose last improvement sits within rounding of loop_loss_reduction may stop one
-    step earlier or later: at most 10 % of the problems, and the others agree as above."""
+    workgroup the two-waypoints-per-lane variant; one trajectory per workgroup padded with idle
+    waves) against the CPU oracle — the reference's fp32 α iteration — on the same problems, 60
+    bench-mode steps or the reference's early exit (loop_loss_reduction 1e-3).  Per checked
+    problem: same step count (faithful mode: a last improvement within rounding of
+    loop_loss_reduction may move the exit by one step — at most 1 in 6), waypoints within
+    max(2·spread, ORACLE_FLOOR) with spread the oracle's own ±1-ulp sensitivity, final loss within 1e-3
+    relative + 3·its ±1-ulp change, and traj_out == K·α_out·J bit for bit."""
     from irm_motion_planning_amd.context import Context
+    from oracle.oracle import Oracle
     argv = ["--optimizer-name", "gd", "--max-outer-iteration", "1", "--n-timesteps", str(N), "--n-joints", str(D)]
     if D != 3:
         argv += ["--link-length"] + [str(3.0 / D)] * D + ["--gd-lr", "1e-3"]
@@ -554,26 +563,21 @@ def test_lean_gd_kernel_matches_general(N, mode, D, tb):
     s = rng.uniform(-0.5, 0.5, (B, D)).astype(np.float32)
     g = rng.uniform(0.2, 1.6, (B, D)).astype(np.float32)
     lean = Context(params(*argv, traj_per_block=tb))
-    os.environ["IRM_GENERAL_KERNEL"] = "1"
-    try:
-        gen = Context(params(*argv, traj_per_block=tb))
-    finally:
-        del os.environ["IRM_GENERAL_KERNEL"]
     a1, t1, st1 = lean.optimize(s, g, obstacles())
-    a2, t2, st2 = gen.optimize(s, g, obstacles())
-    same = st1["inner_iterations"] == st2["inner_iterations"]
-    if mode == "bench":
-        assert same.all()
-    assert same.mean() >= 0.9, same.mean()
-    for k in ("outer_iterations",):
-        np.testing.assert_array_equal(st1[k], st2[k], err_msg=k)
-    np.testing.assert_allclose(t1[same], t2[same], rtol=0, atol=5e-3 if D == 3 else 1e-2)
-    # 2e-4: the λmax > 0 band (a near-tie of two waypoints' costs may pick a different argmax for
-    # one step when the rounding differs; 1–2 of 48 problems move by ≤ 1e-4)
-    np.testing.assert_allclose(st1["final_loss"][same], st2["final_loss"][same], rtol=2e-4)
     np.testing.assert_array_equal(t1, lean.evaluate(a1))  # traj_out == K·α_out·J exactly
-    print(f"N={N} D={D} tb={tb} {mode}: same step counts {same.mean():.2f}, bit-equal {np.mean(np.all(t1 == t2, axis=(1, 2))):.2f}, "
-          f"max |dT| {np.abs(t1[same] - t2[same]).max():.2e}")
+    o = Oracle(params(*argv))
+    moved = 0
+    for b in np.linspace(0, B - 1, 6).astype(int):
+        T, so, spread, lspread = _oracle_band(o, lean.init_alpha(s[b], g[b]), obstacles(), s[b], g[b])
+        if int(st1["grad_evals"][b]) != so["grad_evals"]:
+            assert mode == "faithful" and abs(int(st1["grad_evals"][b]) - so["grad_evals"]) == 1, (b, st1["grad_evals"][b], so)
+            moved += 1
+            continue
+        err = float(np.abs(t1[b] - T).max())
+        print(f"N={N} D={D} tb={tb} {mode} [{b}]: {so['grad_evals']} steps, |traj - oracle| {err:.2e} (spread {spread:.2e})")
+        assert err <= max(2.0 * spread, ORACLE_FLOOR), (b, err, spread)
+        assert abs(float(st1["final_loss"][b]) - so["final_loss"]) <= 1e-3 * abs(so["final_loss"]) + 3 * lspread
+    assert moved <= 1
 
 
 @pytest.mark.parametrize("optimizer,N,B", [("bls", 128, 1), ("bls", 50, 4), ("gd", 128, 8)])
