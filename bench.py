@@ -98,13 +98,15 @@ def make_args(cfg, faithful, max_inner):
 def flops_per_iteration(N, D, O, R):
     """Algorithmic fp32 flops of one GD iteration of one trajectory.
 
-    exec: what the trajectory-space rank-R kernel must do — stage 1 (Fᵀa,
-    2·R·N·D), stage 2 (F·y, 2·2N·R·D), the JᵀJ mix (2·R·D²), the update
-    (4·N·D), obstacle pairs (14·N·O), FK/Jacobian/penalties (24·N·D, sincos
-    counted as 4 flops each).
+    exec: what the lean kernel (k_lean: waypoint-space rank-R iteration with the reference's fp32
+    α rounding) must do — stage 1 (y'' = Fᵀ[a; b]·Jᵀ, 2·R·N·D; the rounding residual z = V_Rᵀ·e',
+    2·R·N·D), stage 2 (F·(y'' + z), 2·2N·R·D; G = V_R·y'', 2·N·R·D), the Jᵀ / J mixes of the
+    gradient inputs and of the direction (2 × 2·2·N·D²), the α update with its error-free
+    residual (14·N·D), the waypoint update (4·N·D), obstacle pairs (14·N·O), FK / Jacobian /
+    penalties (24·N·D, sincos counted as 4 flops each).
     ref: SURVEY.md §8d's count of the reference formulation, 12N²D + 10ND² + 22NO.
     """
-    exec_f = 2 * R * N * D + 4 * N * R * D + 2 * R * D * D + 4 * N * D + 14 * N * O + 24 * N * D
+    exec_f = 10 * R * N * D + 8 * N * D * D + 14 * N * D + 4 * N * D + 14 * N * O + 24 * N * D
     ref_f = 12 * N * N * D + 10 * N * D * D + 22 * N * O
     return exec_f, ref_f
 
@@ -124,11 +126,15 @@ def optimiser_kernel(a, info, N, D, opt, B):
     bt = tb * nw
     if 2 * -(-B // tb) <= info["num_cus"] and bt < 512:
         bt = 512  # small batch: workgroup padded with trajectory-less waves (IRM_PAD_WAVES)
+    if bt < 512:  # lean kernel: at least one wave per stage-1 unit, 256- or 512-thread workgroups
+        bt = max(bt, min(512, 64 * 2 * nsplit))
+        bt = 256 if bt <= 256 else 512
     waves = bt // 64
     wpl = 2 if (nw == 256 and 512 < bt <= 1024) else 1  # N = 256, > 2 trajectories: 2 waypoints/lane
-    lean = (opt == "gd" and not a.faithful and (D, N) in ((3, 50), (3, 64), (3, 128), (3, 256), (7, 128), (7, 256))
-            and info["operator_rank"] == 32 and bt // wpl <= 512 and 2 * nsplit <= waves // wpl)
-    return (f"irm::k_gd_single (GD single loop, {wpl} waypoint(s) per lane; fp32 MFMA 16x16x4 + VALU)" if lean
+    flow = "BLS dual loop" if opt == "bls" else ("GD dual loop" if a.faithful else "GD single loop")
+    lean = ((D, N) in ((3, 50), (3, 64), (3, 128), (3, 256), (7, 128), (7, 256)) and info["operator_rank"] == 32
+            and bt // wpl <= 512 and 2 * nsplit <= waves // wpl and not (opt == "bls" and N > 128))
+    return (f"irm::k_lean ({flow}, {wpl} waypoint(s) per lane; fp32 MFMA 16x16x4 + VALU)" if lean
             else "irm::k_optimize (fp32 MFMA 16x16x4 + VALU)")
 
 

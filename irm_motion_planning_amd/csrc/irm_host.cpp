@@ -311,11 +311,14 @@ int choose_shape(const irm_ctx* c, int B, bool optimizer, KParams& kp, int* lds_
         kp.BT = tb * kp.NW;
         if (pad_ok && 2 * ((B + tb - 1) / tb) <= c->num_cus && kp.BT < 512) kp.BT = 512;
         kp.nsplit = irm::stage1_splits(kp.NK);
-        // the lean GD kernel (k_gd_single) runs one stage-1 unit per wave: small workgroups of a GD
-        // single-loop launch get idle waves up to that count (e.g. one N = 128 trajectory per
-        // workgroup: 2 → 4 waves), so that the lean kernel — and its fp32-α rounding — serves them
-        if (optimizer && kp.optimizer == IRM_OPT_GD && kp.max_outer <= 1 && !kp.record_series)
+        // the lean kernel (k_lean) runs one stage-1 unit per wave and is instantiated for 256- and
+        // 512-thread workgroups: smaller optimiser workgroups get idle waves up to that size (e.g.
+        // one N = 128 trajectory per workgroup: 2 → 4 waves), so that the lean kernel — and its
+        // fp32-α rounding — serves them; the general kernel runs padded workgroups bit-identically
+        if (optimizer && kp.BT < 512) {
             kp.BT = std::max(kp.BT, std::min(512, 64 * (kp.RP / 16) * kp.nsplit));
+            kp.BT = kp.BT <= 256 ? 256 : 512;
+        }
         if (optimizer) {
             kp.regops = irm::regops_fit(kp) ? 1 : 0;
             irm::Plan a = irm::plan_lds(kp, true, true);
@@ -663,9 +666,10 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
     kp.eps_v = p->eps_velocity;
     kp.lmax = p->lambda_max_cost;
     kp.lreg = p->lambda_reg;
-    // GD single loop's weight decay (1 − λ_reg·lr): Python floats, cast to fp32 where they meet α
-    // (optimizer_GD.py:81)
-    kp.gd_c0 = (float)(1.0 - decimal_double(p->lambda_reg) * decimal_double(p->gd_lr[0]));
+    // GD weight decay (1 − λ_reg·lr) per outer iteration: Python floats, cast to fp32 where they
+    // meet α (optimizer_GD.py:81, :185)
+    for (int i = 0; i < IRM_MAX_LR; ++i)
+        kp.gd_c[i] = (float)(1.0 - decimal_double(p->lambda_reg) * decimal_double(p->gd_lr[i]));
     kp.bls_lr0 = p->bls_lr_start;
     kp.bls_a = p->bls_alpha;
     kp.bls_bp = p->bls_beta_plus;

@@ -43,12 +43,13 @@ struct KParams {
     int32_t lean_ok;  // k_gd_single may serve GD single-loop launches (IRM_GENERAL_KERNEL=1 clears it)
     int32_t lean_wpl; // diagnostics: IRM_LEAN_WPL=2 forces two waypoints per lane at N ≤ 128
     float llr, lci, lsg0, ljl0, eps_p, eps_v, lmax, lreg;
-    float bls_lr0, bls_a, bls_bp, bls_bm, vmax, pmax, pmin, gd_c0;  // gd_c0 = fp32(1 − λ_reg·lr₀) from doubles
+    float bls_lr0, bls_a, bls_bp, bls_bm, vmax, pmax, pmin, pad1;
     // derived fp32 constants (reference casts its Python doubles to fp32)
     float mean_pos, std_pos, std2, vmax2, thr_hi, thr_lo, thr_v, invN;
     float inv_std_pos, inv_vmax, inv_std2, inv_vmax2;  // reciprocals: x/c → x·(1/c) in the hot loops
     uint32_t Nmagic, NDmagic;  // ⌈2³²/N⌉, ⌈2³²/(N·D)⌉: exact __umulhi division for dividends < 2¹⁶
     float gd_lr[IRM_MAX_LR];
+    float gd_c[IRM_MAX_LR];  // GD weight decay fp32(1 − λ_reg·lr_k), from the Python doubles (optimizer_GD.py:81)
     float link[IRM_MAX_JOINTS];
     float J[IRM_MAX_JOINTS * IRM_MAX_JOINTS];    // J (D×D, row-major, stride D)
     float JtJ[IRM_MAX_JOINTS * IRM_MAX_JOINTS];  // JᵀJ
@@ -218,11 +219,13 @@ __host__ __device__ inline Plan plan_lds(const KParams& p, bool ops_lds, bool op
 // endpoint operator columns hL (2·MP), G's endpoint columns hV (2·NK), the V_R fragments (when
 // staged: vlds), the rounding residual rows e' ([column][waypoint], stride NK + 8), its stage-1
 // partials zp ([split][column][r], stride RP + 8) and the gradient rows G ([column][waypoint]).
+// With the BLS flow also dc: F·(V_Rᵀ·e) [column][row] (stride MP + 8), the rounding residual's
+// waypoint-space correction (the line search's trial steps cannot carry it folded into y'').
 struct LeanX {
-    int hl, hv, vt, vn, eb, zp, gb, total;
+    int hl, hv, vt, vn, eb, zp, gb, dc, total;
 };
 __host__ __device__ constexpr int lean_ld(int NK) { return NK + 8; }
-__host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, int nsplit, bool vlds) {
+__host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, int nsplit, bool vlds, bool bls = false) {
     LeanX e{};
     int off = base;
     e.hl = off;
@@ -242,6 +245,11 @@ __host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, in
     off += al4(nsplit * 16 * (RP + 8));
     e.gb = off;
     off += al4(16 * lean_ld(NK));
+    e.dc = 0;
+    if (bls) {
+        e.dc = off;
+        off += al4(16 * (MP + 8));
+    }
     e.total = off;
     return e;
 }

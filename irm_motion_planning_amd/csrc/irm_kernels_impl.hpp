@@ -469,9 +469,11 @@ __device__ void stage_alpha(const KParams& P, int tb0, int ntb, float* X, int xr
 //
 // Lane n of trajectory column block Xa (LDS, rows m = 0..N-1, stride kLd):
 //   q = fp32(fp32(K·α)[n]·J), v = fp32(fp32(dK·α)[n]·J).
+// (rs, cs: row / column strides of Xa — [row][16] LDS buffers by default, the lean kernel's
+// column-major buffers with rs = 1, cs = column stride)
 template <int D>
 __device__ void eval_exact(const KParams& P, const float* __restrict__ Xa, int n, float (&q)[D], float (&v)[D],
-                           const float* Kt = nullptr, const float* dKt = nullptr) {
+                           const float* Kt = nullptr, const float* dKt = nullptr, int rs = kLd, int cs = 1) {
     const int N = P.N;
     double aq[D], av[D];
 #pragma unroll
@@ -480,10 +482,10 @@ __device__ void eval_exact(const KParams& P, const float* __restrict__ Xa, int n
     const float* dkt = (dKt ? dKt : P.dKt) + n;
     for (int m = 0; m < N; ++m) {
         const double kq = (double)kt[(size_t)m * N], kv = (double)dkt[(size_t)m * N];  // K[n][m], dK[n][m]
-        const float* xr = Xa + m * kLd;
+        const float* xr = Xa + m * rs;
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            const double x = (double)xr[d];
+            const double x = (double)xr[d * cs];
             aq[d] = fma(kq, x, aq[d]);
             av[d] = fma(kv, x, av[d]);
         }
@@ -1470,11 +1472,19 @@ __device__ __forceinline__ float alpha_step(float al, float c, float lr, float g
     return an;
 }
 
+// Control flows of the lean kernel: the GD single loop (optimizer_GD.py:68-97, the bench path), the
+// GD dual loop (optimizer_GD.py:173-232) and the BLS dual loop (optimizer_BLS.py:127-213).
+enum LeanFlow : int { LF_GD1 = 0, LF_GD2 = 1, LF_BLS = 2 };
+// Per-trajectory phase (LF_GD2 / LF_BLS): a GD step or BLS trial this round, the end of an inner
+// loop (α's exact trajectory, constraintsFulfilled, λ escalation), done.
+enum LeanPhase : int { LP_STEP = 0, LP_RESYNC = 1, LP_DONE = 2 };
+
 // FULL: the launch has exactly MAXT threads, so the stage-2 tiles per wave are known exactly
 // (otherwise kS2T(MAXT) bounds them for smaller launches): C7's 256-thread variant then holds 4
 // tiles of operator fragments instead of 8 (32 VGPRs) and does not spill.
-template <class S, int MAXT, int WPL, bool FULL = false>
-__global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_single(KParams P) {
+template <class S, int MAXT, int WPL, bool FULL = false, int FLOW = LF_GD1>
+__global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lean(KParams P) {
+    constexpr bool GD1 = FLOW == LF_GD1, BLS = FLOW == LF_BLS;
     constexpr int D = S::D;
     constexpr int S1Q = kS1Q(MAXT);
     // stage-2 tiles per wave: all of this shape's tiles over the workgroup's waves (N = 256: 4)
@@ -1507,6 +1517,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
         vl[j] = tvalid && nn[j] < N;
     }
     const size_t b = (size_t)(tb0 + (tvalid ? t : 0));
+    const bool rec = !GD1 && P.record_series && P.series;
     Prof prof;
     if (tid == 0) prof.init();
 
@@ -1515,15 +1526,17 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
     float* Ypart = smem + H.Ypart;
     float* red = smem + H.red;
     float* sg = smem + H.sg;
+    float* wp = smem + H.wp;
     unsigned* fw = reinterpret_cast<unsigned*>(smem + H.flags);
     float* obsL = smem + H.obs;
     const int nsplit = sh.NSPLIT;
-    const LeanX LX = lean_extra(plan_lds(P, false, true).total, MP, NK, RP, nsplit, VL);
+    const LeanX LX = lean_extra(plan_lds(P, false, true).total, MP, NK, RP, nsplit, VL, BLS);
     float* hL = smem + LX.hl;  // endpoint columns of F·Fᵀ (2·MP), read per round when WPL > 1
     float* hVL = smem + LX.hv; // G's endpoint columns (2·NK), read per round when WPL > 1
     float* Eb = smem + LX.eb;  // e' rows [column][waypoint]
     float* Zp = smem + LX.zp;  // stage-1 partials of V_Rᵀ·e'
-    float* Gb = smem + LX.gb;  // (V_R·y')[waypoint] rows [column][waypoint]
+    float* Gb = smem + LX.gb;  // (V_R·y'')[waypoint] rows [column][waypoint]
+    float* dC = smem + LX.dc;  // BLS: F·(V_Rᵀ·e) rows [column][row]
     const float* VT = VL ? smem + LX.vt : P.VTp;
     const float* VN = VL ? smem + LX.vn : P.VNp;
 
@@ -1570,6 +1583,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
         hv0[j] = (vl[j] && !kHL) ? P.HV[nn[j]] : 0.f;
         hv1[j] = (vl[j] && !kHL) ? P.HV[NK + nn[j]] : 0.f;
     }
+    // BLS: F's endpoint velocity rows for the ‖G‖ / alpha_norm rows r = li < RP
+    const float fb0 = (BLS && tvalid && li < RP) ? P.Fbot[li] : 0.f;
+    const float fb1 = (BLS && tvalid && li < RP) ? P.Fbot[(size_t)(N - 1) * RP + li] : 0.f;
     if constexpr (kHL) {
         for (int e = tid; e < 2 * MP; e += P.BT) hL[e] = P.Hend[e];
         for (int e = tid; e < 2 * NK; e += P.BT) hVL[e] = P.HV[e];
@@ -1605,23 +1621,36 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
             q[j][k] = v[j][k] = 0.f;
             al[j][k] = vl[j] ? X[nn[j] * kLd + t * D + k] : 0.f;
         }
-        if (vl[j]) eval_exact<D>(P, X + t * D, nn[j], q[j], v[j]);
+        if (vl[j]) {
+            eval_exact<D>(P, X + t * D, nn[j], q[j], v[j]);
+            if (rec) {  // series frame 0: the initial trajectory
+#pragma unroll
+                for (int k = 0; k < D; ++k) P.series[(b * P.max_series) * N * D + nn[j] * D + k] = q[j][k];
+            }
+        }
     }
     __syncthreads();
     for (int e = tid; e < MP * kLd; e += P.BT) X[e] = 0.f;
     const float* obs = obsL + (P.obs_stride ? t * obs_pitch(P.O) : 0);
-    const float lsg = P.lsg0, ljl = P.ljl0, lr = P.gd_lr[0];
-    const float cfac = P.gd_c0, step = lr;
-    const float nilr = -1.f / lr;  // e' = −e/lr: the update then adds −lr·(F·V_Rᵀe')·J = L·e·J
+    // replicated per-trajectory state
+    float lsg = P.lsg0, ljl = P.ljl0;
+    float lr = BLS ? P.bls_lr0 : P.gd_lr[0];
+    float cfac = P.gd_c[0];  // GD: fp32(1 − λ_reg·lr) of the outer iteration
+    float gnorm = 1.f, anorm = 0.f;  // BLS: ‖G‖ and alpha_norm of the current direction
+    int outer = 0, inner = 0, trial = 0;
+    int phase = tvalid ? LP_STEP : LP_DONE;
+    bool needs_dir = false, xdense = false;
+    const float nilr = -1.f / lr;  // GD single loop: e' = −e/lr (the dual loop recomputes per outer)
 
     // evaluation of (q2, v2) with this trajectory's waves: wave partials + endpoint rows
-    auto evaluate = [&](const float (&q2)[WPL][D], const float (&v2)[WPL][D], bool ext, WP<D> (&w)[WPL]) {
+    auto evaluate = [&](const float (&q2)[WPL][D], const float (&v2)[WPL][D], bool ext, float ljl_e,
+                        WP<D> (&w)[WPL]) {
         float cvs[WPL], us = 0.f, tx = -INFINITY, tn = INFINITY, va = 0.f;
 #pragma unroll
         for (int j = 0; j < WPL; ++j) {
             if (vl[j]) eval_waypoint<D>(P, q2[j], v2[j], obs, w[j]);
             cvs[j] = w[j].cv;
-            const float u = P.one_m_lmax * (w[j].cv * P.invN) + ljl * ((w[j].jp + w[j].jv) * P.invN);
+            const float u = P.one_m_lmax * (w[j].cv * P.invN) + ljl_e * ((w[j].jp + w[j].jv) * P.invN);
             if (j == 0) {
                 us = u;
                 tx = w[j].tx;
@@ -1656,7 +1685,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
         float nl, tx, tn, va, a0, b0, a1, b1;
         int idx;
     };
-    auto finalize = [&]() {
+    auto finalize = [&](float lsg_e) {
         const float* r0 = red + (t * WPTL) * 8;
         float cmax = r0[0];
         int cidx = __float_as_int(r0[1]);
@@ -1676,7 +1705,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
         f.b1 = sg[t * 4 + 3];
         const float sgpc = 0.5f * f.a0 + 0.5f * f.a1;  // trajectory.py:187
         const float sgvc = 0.5f * f.b0 + 0.5f * f.b1;  // trajectory.py:203
-        f.nl = (P.lam_max * cmax + usum) + lsg * (sgpc + sgvc);
+        f.nl = (P.lam_max * cmax + usum) + lsg_e * (sgpc + sgvc);
         f.idx = cidx;
         f.tx = tx;
         f.tn = tn;
@@ -1684,14 +1713,15 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
         return f;
     };
     // gradient inputs at (q2, v2), mixed by Jᵀ, into X; returns "b' non-zero away from the endpoints"
-    auto grad_inputs = [&](const WP<D> (&w)[WPL], const float (&q2)[WPL][D], const float (&v2)[WPL][D], int cidx) {
+    auto grad_inputs = [&](const WP<D> (&w)[WPL], const float (&q2)[WPL][D], const float (&v2)[WPL][D], int cidx,
+                           float lsg_e, float ljl_e) {
         bool bfar = false;
 #pragma unroll
         for (int j = 0; j < WPL; ++j) {
             const int n = nn[j];
             if (vl[j]) {
                 float a[D], bb[D];
-                grad_waypoint<D>(P, w[j], q2[j], v2[j], n, cidx, lsg, ljl, s, g, a, bb);
+                grad_waypoint<D>(P, w[j], q2[j], v2[j], n, cidx, lsg_e, ljl_e, s, g, a, bb);
                 const bool endrow = (n == 0 || n == N - 1);
 #pragma unroll
                 for (int k = 0; k < D; ++k) {
@@ -1782,31 +1812,175 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
             *reinterpret_cast<f32x4*>(Zp + (sp * 16 + cl) * ldy + tile * 16 + r4) = acc0 + acc1;
         }
     };
+    // stage 2: dP = F·(Σ_s Ypart[s] (+ Σ_s Zp[s]: GD, the folded residual)), Gb = V_R·Σ_s Ypart[s];
+    // BLS: dC = F·Σ_s Zp[s] separately
+    auto stage2 = [&]() {
+        f32x4 acc[S2T], acz[BLS ? S2T : 1];
+#pragma unroll
+        for (int j = 0; j < S2T; ++j) {
+            acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if constexpr (BLS) acz[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        f32x4 by[2], bt[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            by[i] = bt[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (i < KQ2) {
+                f32x4 bz = {0.f, 0.f, 0.f, 0.f};
+                for (int sp = 0; sp < nsplit; ++sp) {
+                    by[i] += *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + cl) * ldy + i * 16 + r4);
+                    bz += *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + i * 16 + r4);
+                }
+                bt[i] = BLS ? bz : by[i] + bz;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            if (i < KQ2) {
+#pragma unroll
+                for (int j = 0; j < S2T; ++j) {
+                    if (wave + j * nwaves < MT2) {
+                        const f32x4 bd = BLS ? by[i] : bt[i];
+#pragma unroll
+                        for (int m = 0; m < 4; ++m)
+                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][m], bd[m], acc[j], 0, 0, 0);
+                        if constexpr (BLS) {
+#pragma unroll
+                            for (int m = 0; m < 4; ++m)
+                                acz[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][m], bt[i][m], acz[j], 0, 0, 0);
+                        }
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < S2T; ++j) {
+            if (wave + j * nwaves < MT2) {
+                *reinterpret_cast<f32x4*>(dP + cl * ldx + (wave + j * nwaves) * 16 + r4) = acc[j];
+                if constexpr (BLS) *reinterpret_cast<f32x4*>(dC + cl * ldx + (wave + j * nwaves) * 16 + r4) = acz[j];
+            }
+        }
+        // G tiles (waypoint rows of V_R·y''), from the top wave down
+        for (int u = nwaves - 1 - wave; u < MTG; u += nwaves) {
+            const f32x4* ap = reinterpret_cast<const f32x4*>(VN) + (size_t)u * KQ2 * 64 + lane;
+            f32x4 ag = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                if (i < KQ2) {
+                    const f32x4 a = ap[(size_t)i * 64];
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) ag = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], by[i][m], ag, 0, 0, 0);
+                }
+            }
+            *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4) = ag;
+        }
+    };
+    // this lane's direction rows Δ = (F·y'')·J for waypoint j (endpoint velocity rows through
+    // their operator columns: stage 1's operator has zero columns there)
+    auto direction = [&](int j, const float (&e0)[D], const float (&e1)[D], float (&dt)[D], float (&dv)[D]) {
+        float ut[D], uv[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            ut[k] = dP[(t * D + k) * ldx + nn[j]];
+            uv[k] = dP[(t * D + k) * ldx + NK + nn[j]];
+            if constexpr (kHL) {
+                const int r = vl[j] ? nn[j] : 0;
+                ut[k] = fmaf(hL[r], e0[k], fmaf(hL[MP + r], e1[k], ut[k]));
+                uv[k] = fmaf(hL[NK + r], e0[k], fmaf(hL[MP + NK + r], e1[k], uv[k]));
+            } else {
+                ut[k] = fmaf(h0T[j], e0[k], fmaf(h1T[j], e1[k], ut[k]));
+                uv[k] = fmaf(h0V[j], e0[k], fmaf(h1V[j], e1[k], uv[k]));
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            float a = 0.f, c = 0.f;
+#pragma unroll
+            for (int l = 0; l < D; ++l) {
+                a = fmaf(ut[l], P.J[l * D + k], a);
+                c = fmaf(uv[l], P.J[l * D + k], c);
+            }
+            dt[k] = a;
+            dv[k] = c;
+        }
+    };
+    // G[n] = (V_R·y'')[n] + G's endpoint velocity columns (no mix: [a'; b'] carry Jᵀ)
+    auto grad_alpha = [&](int j, const float (&e0)[D], const float (&e1)[D], float (&G)[D]) {
+        const int r = vl[j] ? nn[j] : 0;
+        const float v0 = kHL ? hVL[r] : hv0[j], v1 = kHL ? hVL[NK + r] : hv1[j];
+#pragma unroll
+        for (int k = 0; k < D; ++k) G[k] = fmaf(v0, e0[k], fmaf(v1, e1[k], Gb[(t * D + k) * lde + r]));
+    };
+    auto snapshot = [&](irm_stats& st) {  // extended-vis frame after a non-breaking inner iteration
+        if (rec && st.series_len < P.max_series) {
+#pragma unroll
+            for (int j = 0; j < WPL; ++j) {
+                if (vl[j]) {
+#pragma unroll
+                    for (int k = 0; k < D; ++k)
+                        P.series[((b * P.max_series) + st.series_len) * N * D + nn[j] * D + k] = q[j][k];
+                }
+            }
+            st.series_len++;
+        }
+    };
 
-    // round 0 (optimizer_GD.py:93: the loss at α0) and the first gradient inputs
+    // round 0 (optimizer_GD.py:93 / :210: the loss at α0) and the first gradient inputs
     irm_stats st{};
+    st.series_len = rec ? 1 : 0;
     float loss;
     bool done = !tvalid;
     {
         WP<D> w[WPL];
-        evaluate(q, v, false, w);
+        evaluate(q, v, false, ljl, w);
         __syncthreads();
-        const Fin f = finalize();
+        const Fin f = finalize(lsg);
         loss = f.nl;
-        st.cost_evals = 1;
-        if (P.max_inner <= 0) done = true;
-        const bool bfar = grad_inputs(w, q, v, f.idx);
-        if (lane == 0 && (!done || bfar)) atomicOr(&fw[0], (done ? 0u : 1u << wave) | (bfar ? 1u << 31 : 0u));
+        if constexpr (!BLS) st.cost_evals = 1;
+        bool to_end = P.max_inner <= 0;
+        // BLS with max_outer_iteration <= 0: the outer while_loop never runs and α0 is returned
+        // (optimizer_BLS.py:184-186, 210-213): straight to the constraint check
+        if constexpr (BLS) to_end = to_end || P.max_outer <= 0;
+        bool bfar = false;
+        if constexpr (GD1) {
+            if (to_end) done = true;
+        } else if (to_end) {
+            phase = LP_RESYNC;
+            st.final_loss = loss;
+        } else {
+            needs_dir = true;
+        }
+        if (!done && !to_end) {
+            bfar = grad_inputs(w, q, v, f.idx, lsg, ljl);
+            xdense = bfar;
+        }
+        if constexpr (GD1) {
+            if (lane == 0 && (!done || bfar)) atomicOr(&fw[0], (done ? 0u : 1u << wave) | (bfar ? 1u << 31 : 0u));
+        } else {
+            if (lane == 0 && tvalid)
+                atomicOr(&fw[0], (1u << wave) | (needs_dir ? 1u << 28 : 0u) | (phase == LP_RESYNC ? 1u << 29 : 0u) |
+                                     (bfar ? 1u << 31 : 0u));
+        }
     }
     __syncthreads();
 
     IRM_STAMP(14);
-    // ---------------------------------------------------------- GD rounds
-    int inner = 0;
+    // ---------------------------------------------------------- rounds
+    float dTl[BLS ? WPL : 1][D], dVl[BLS ? WPL : 1][D], Gl[BLS ? WPL : 1][D];  // BLS: latched direction
+#pragma unroll
+    for (int j = 0; j < (BLS ? WPL : 1); ++j)
+#pragma unroll
+        for (int k = 0; k < D; ++k) dTl[j][k] = dVl[j][k] = Gl[j][k] = 0.f;
     for (int par = 0;; par ^= 1) {
         const unsigned fl = fw[par];
-        if ((fl & 0x7FFFFFFFu) == 0u) break;  // every trajectory of the block is done
+        if constexpr (GD1) {
+            if ((fl & 0x7FFFFFFFu) == 0u) break;  // every trajectory of the block is done
+        } else {
+            if ((fl & 0xFFFFu) == 0u) break;
+        }
         const bool dense = (fl >> 31) != 0u;
+        const bool dirr = GD1 || ((fl >> 28) & 1u);  // some trajectory needs a direction this round
+        const bool rsy = !GD1 && ((fl >> 29) & 1u);  // some trajectory ends an inner loop this round
         if (tid == 0) fw[par ^ 1] = 0u;
         // the endpoint velocity rows of this trajectory's gradient inputs (their operator columns)
         float e0[D], e1[D];
@@ -1817,102 +1991,153 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
             e1[k] = xc[NK + N - 1];
         }
         IRM_STAMP(0);
-        IRM_COUNT(13, dense);
-        stage1(dense);
-        stage1z();
-        IRM_STAMP(1);
-        __syncthreads();
-        IRM_STAMP(2);
-        {  // stage 2: dP = F·(Σ_s Ypart[s] + Σ_s Zp[s]), Gb = V_R·Σ_s Ypart[s]
-            f32x4 acc[S2T];
+        if (dirr) {  // block-uniform
+            IRM_COUNT(13, dense);
+            stage1(dense);
+            stage1z();
+            IRM_STAMP(1);
+            __syncthreads();
+            IRM_STAMP(2);
+            if constexpr (BLS) {
+                // ‖G‖² = ‖ŷ‖², alpha_norm·‖G‖ = Σ_r (ŷ_r·1)² with G = V_R·ŷ, ŷ = y'' + the endpoint
+                // velocity rows (optimizer_BLS.py:165-166 without forming G), rows r = li < RP of the
+                // trajectory's first wave
+                if (needs_dir && n0 == 0) {  // wave-uniform
+                    float g2 = 0.f, s1 = 0.f;
+                    if (tvalid && li < RP) {
+                        float sa = 0.f;
 #pragma unroll
-            for (int j = 0; j < S2T; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-            f32x4 by[2], bt[2];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                by[i] = bt[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-                if (i < KQ2) {
-                    f32x4 bz = {0.f, 0.f, 0.f, 0.f};
-                    for (int sp = 0; sp < nsplit; ++sp) {
-                        by[i] += *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + cl) * ldy + i * 16 + r4);
-                        bz += *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + i * 16 + r4);
+                        for (int a = 0; a < D; ++a) {
+                            float y = fmaf(fb0, e0[a], fb1 * e1[a]);
+                            for (int sp = 0; sp < nsplit; ++sp) y += Ypart[(sp * 16 + t * D + a) * ldy + li];
+                            g2 = fmaf(y, y, g2);
+                            sa += y;
+                        }
+                        s1 = sa * sa;
                     }
-                    bt[i] = by[i] + bz;
+                    g2 = wred_sum(g2);
+                    s1 = wred_sum(s1);
+                    if (lane == 0) {
+                        wp[t * 2] = g2;
+                        wp[t * 2 + 1] = s1;
+                    }
                 }
             }
+            stage2();
+            IRM_STAMP(3);
+            __syncthreads();
+            IRM_STAMP(4);
+        }
+        // ------------------------------------------------ BLS: latch the direction
+        if constexpr (BLS) {
+            if (needs_dir) {  // wave-uniform; the inner-loop head (optimizer_BLS.py:163-166)
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                if (i < KQ2) {
+                for (int j = 0; j < WPL; ++j) {
+                    direction(j, e0, e1, dTl[j], dVl[j]);
+                    grad_alpha(j, e0, e1, Gl[j]);
+                    // the pending rounding residual of the last accepted trial: [T; V] += L·e·J
+                    float ct[D], cv[D];
 #pragma unroll
-                    for (int j = 0; j < S2T; ++j) {
-                        if (wave + j * nwaves < MT2) {
-                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][0], bt[i][0], acc[j], 0, 0, 0);
-                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][1], bt[i][1], acc[j], 0, 0, 0);
-                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][2], bt[i][2], acc[j], 0, 0, 0);
-                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][3], bt[i][3], acc[j], 0, 0, 0);
+                    for (int k = 0; k < D; ++k) {
+                        ct[k] = dC[(t * D + k) * ldx + nn[j]];
+                        cv[k] = dC[(t * D + k) * ldx + NK + nn[j]];
+                    }
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        float a = 0.f, c = 0.f;
+#pragma unroll
+                        for (int l = 0; l < D; ++l) {
+                            a = fmaf(ct[l], P.J[l * D + k], a);
+                            c = fmaf(cv[l], P.J[l * D + k], c);
+                        }
+                        q[j][k] += a;
+                        v[j][k] += c;
+                        if (vl[j]) Eb[(t * D + k) * lde + nn[j]] = 0.f;  // consumed
+                    }
+                }
+                gnorm = sqrtf(wp[t * 2]);
+                anorm = wp[t * 2 + 1] / gnorm;
+                st.grad_evals++;  // cost + grad at α (optimizer_BLS.py:163-164)
+                st.cost_evals++;
+                trial = 0;
+                needs_dir = false;
+            }
+        }
+        // ------------------------------------------------ end of an inner loop: α's exact trajectory
+        if (rsy) {  // block-uniform
+            const bool rs = phase == LP_RESYNC;  // wave-uniform
+            if (rs) {
+#pragma unroll
+                for (int j = 0; j < WPL; ++j) {
+                    if (vl[j]) {
+#pragma unroll
+                        for (int k = 0; k < D; ++k) {
+                            X[(t * D + k) * ldx + nn[j]] = al[j][k];
+                            Eb[(t * D + k) * lde + nn[j]] = 0.f;  // absorbed by the exact trajectory
                         }
                     }
                 }
             }
+            __syncthreads();
+            if (rs) {
 #pragma unroll
-            for (int j = 0; j < S2T; ++j)
-                if (wave + j * nwaves < MT2)
-                    *reinterpret_cast<f32x4*>(dP + cl * ldx + (wave + j * nwaves) * 16 + r4) = acc[j];
-            // G tiles (waypoint rows of V_R·y'), from the top wave down
-            for (int u = nwaves - 1 - wave; u < MTG; u += nwaves) {
-                const f32x4* ap = reinterpret_cast<const f32x4*>(VN) + (size_t)u * KQ2 * 64 + lane;
-                f32x4 ag = {0.f, 0.f, 0.f, 0.f};
+                for (int j = 0; j < WPL; ++j) {
+                    if (vl[j]) {
+                        eval_exact<D>(P, X + (t * D) * ldx, nn[j], q[j], v[j], nullptr, nullptr, 1, ldx);
+                        // the last extended-vis frame shows the exact trajectory of the returned α
+                        if (rec && st.series_len > 0) {
 #pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    if (i < KQ2) {
-                        const f32x4 a = ap[(size_t)i * 64];
-                        ag = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], by[i][0], ag, 0, 0, 0);
-                        ag = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], by[i][1], ag, 0, 0, 0);
-                        ag = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], by[i][2], ag, 0, 0, 0);
-                        ag = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], by[i][3], ag, 0, 0, 0);
+                            for (int k = 0; k < D; ++k)
+                                P.series[((b * P.max_series) + st.series_len - 1) * N * D + nn[j] * D + k] = q[j][k];
+                        }
                     }
                 }
-                *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4) = ag;
             }
+            __syncthreads();  // X is rewritten by this round's gradient inputs
         }
-        IRM_STAMP(3);
-        __syncthreads();
-        IRM_STAMP(4);
+        // ------------------------------------------------ update + evaluate
         float q2[WPL][D], v2[WPL][D];
+        float cj = cfac, stepj = lr;  // this round's step (BLS: the trial's)
+        const float lrj = lr;
+        if constexpr (BLS) {
+            cj = unfused(1.f - unfused(P.lreg * lr));  // (1 − λ_reg·bls_lr) in fp32 (optimizer_BLS.py:139)
+            stepj = lr / gnorm;
+        }
         WP<D> w[WPL];
-        if (!done) {  // wave-uniform
+        const bool stepping = GD1 ? !done : phase == LP_STEP;  // wave-uniform
+        const bool ev = GD1 ? !done : phase != LP_DONE;
+        if (ev) {
 #pragma unroll
             for (int j = 0; j < WPL; ++j) {
-                float ut[D], uv[D];
+                if (stepping) {
+                    float dt[D], dv[D];
+                    if constexpr (BLS) {
 #pragma unroll
-                for (int k = 0; k < D; ++k) {
-                    ut[k] = dP[(t * D + k) * ldx + nn[j]];
-                    uv[k] = dP[(t * D + k) * ldx + NK + nn[j]];
-                    // endpoint velocity rows enter through their operator columns in every round
-                    // (stage 1's operator has zero columns there: a dense round adds exact zeros)
-                    if constexpr (kHL) {
-                        const int r = vl[j] ? nn[j] : 0;
-                        ut[k] = fmaf(hL[r], e0[k], fmaf(hL[MP + r], e1[k], ut[k]));
-                        uv[k] = fmaf(hL[NK + r], e0[k], fmaf(hL[MP + NK + r], e1[k], uv[k]));
+                        for (int k = 0; k < D; ++k) {
+                            dt[k] = dTl[j][k];
+                            dv[k] = dVl[j][k];
+                        }
                     } else {
-                        ut[k] = fmaf(h0T[j], e0[k], fmaf(h1T[j], e1[k], ut[k]));
-                        uv[k] = fmaf(h0V[j], e0[k], fmaf(h1V[j], e1[k], uv[k]));
+                        direction(j, e0, e1, dt, dv);
                     }
-                }
 #pragma unroll
-                for (int k = 0; k < D; ++k) {  // Δ[T; V] = (F·y'')·J
-                    float dt = 0.f, dv = 0.f;
-#pragma unroll
-                    for (int l = 0; l < D; ++l) {
-                        dt = fmaf(ut[l], P.J[l * D + k], dt);
-                        dv = fmaf(uv[l], P.J[l * D + k], dv);
+                    for (int k = 0; k < D; ++k) {
+                        q2[j][k] = cj * q[j][k] - stepj * dt[k];
+                        v2[j][k] = cj * v[j][k] - stepj * dv[k];
                     }
-                    q2[j][k] = cfac * q[j][k] - step * dt;
-                    v2[j][k] = cfac * v[j][k] - step * dv;
+                } else {
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        q2[j][k] = q[j][k];
+                        v2[j][k] = v[j][k];
+                    }
                 }
             }
             IRM_STAMP(5);
-            evaluate(q2, v2, false, w);
+            // an inner loop's end is evaluated with the next outer iteration's λ (its loss and gradient
+            // start that iteration; the constraint terms do not depend on λ)
+            const bool rs = !GD1 && phase == LP_RESYNC;
+            evaluate(q2, v2, rs, rs ? ljl * P.lci : ljl, w);
         }
         IRM_STAMP(7);
         if constexpr (WPTL > 1) {
@@ -1922,39 +2147,164 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
             asm volatile("" ::: "memory");
         }
         IRM_STAMP(8);
-        if (!done) {
-            const Fin f = finalize();
+        if (ev) {
+            const bool rs = !GD1 && phase == LP_RESYNC;
+            const float lsg_e = rs ? lsg * P.lci : lsg;
+            const Fin f = finalize(lsg_e);
             IRM_STAMP(9);
-            st.grad_evals++;
-            st.cost_evals++;
-            bool bfar = false;
-            if (loss - f.nl < P.llr) {
-                done = true;  // minimized: the step is discarded (optimizer_GD.py:87-90)
-            } else {
-                // accepted: α' = fl(fl(c·α) − fl(lr·G)) (optimizer_GD.py:81) and its residual e' for
-                // the next round's stage 1
-#pragma unroll
-                for (int j = 0; j < WPL; ++j) {
-                    const int r = vl[j] ? nn[j] : 0;
-                    const float v0 = kHL ? hVL[r] : hv0[j], v1 = kHL ? hVL[NK + r] : hv1[j];
-#pragma unroll
-                    for (int k = 0; k < D; ++k) {
-                        const float G = fmaf(v0, e0[k], fmaf(v1, e1[k], Gb[(t * D + k) * lde + r]));
-                        float er;
-                        al[j][k] = alpha_step(al[j][k], cfac, lr, G, step, G, er);
-                        q[j][k] = q2[j][k];
-                        v[j][k] = v2[j][k];
-                        if (vl[j]) Eb[(t * D + k) * lde + nn[j]] = nilr * er;
+            bool bfar = false, to_end = false, accept = false, snap = false, more = false;
+            if constexpr (!BLS) needs_dir = false;  // GD: every step consumes its direction
+            if constexpr (GD1) {
+                st.grad_evals++;
+                st.cost_evals++;
+                if (loss - f.nl < P.llr) {
+                    done = true;  // minimized: the step is discarded (optimizer_GD.py:87-90)
+                } else {
+                    accept = true;
+                    loss = f.nl;
+                    inner++;
+                    st.inner_iterations++;
+                    if (inner >= P.max_inner) done = true;
+                    else more = true;
+                }
+            } else if (rs) {
+                // constraintsFulfilled(α) (trajectory.py:129-137, robot.py:90-113) on α's exact
+                // trajectory; optimizer_GD.py:214-224 / optimizer_BLS.py:196-208
+                const bool ok = sqrtf(f.a0) < P.eps_p && sqrtf(f.a1) < P.eps_p && sqrtf(f.b0) < P.eps_v &&
+                                sqrtf(f.b1) < P.eps_v && f.tx <= P.pmax && f.tn >= P.pmin && f.va <= P.vmax;
+                if (!BLS || P.max_outer > 0) st.outer_iterations++;
+                st.constraints_ok = ok ? 1 : 0;
+                outer++;
+                if (ok || outer >= P.max_outer) {
+                    phase = LP_DONE;
+                } else {  // next outer iteration: λ escalated, lr reset, loss at α (optimizer_GD.py:210)
+                    lsg = lsg_e;
+                    ljl = ljl * P.lci;
+                    loss = f.nl;
+                    inner = 0;
+                    if constexpr (BLS) {
+                        lr = P.bls_lr0;
+                    } else {
+                        lr = P.gd_lr[outer];
+                        cfac = P.gd_c[outer];
+                        st.cost_evals++;
+                    }
+                    if (P.max_inner <= 0) {
+                        st.final_loss = loss;  // phase stays LP_RESYNC: the empty inner loop ends at once
+                    } else {
+                        phase = LP_STEP;
+                        more = true;
                     }
                 }
-                loss = f.nl;
-                inner++;
-                st.inner_iterations++;
-                if (inner >= P.max_inner) done = true;
-                else bfar = grad_inputs(w, q2, v2, f.idx);
+            } else if constexpr (!BLS) {  // GD dual loop inner step (optimizer_GD.py:180-195)
+                st.grad_evals++;
+                st.cost_evals++;
+                if (loss - f.nl < P.llr) {
+                    to_end = true;  // minimized: the step is discarded
+                } else {
+                    accept = true;
+                    snap = true;
+                    loss = f.nl;
+                    inner++;
+                    st.inner_iterations++;
+                    if (inner >= P.max_inner) to_end = true;
+                    else more = true;
+                }
+            } else {  // BLS trial (optimizer_BLS.py:136-150, 172-178)
+                st.cost_evals++;
+                st.bls_trials++;
+                const float required = loss - P.bls_a * lr * anorm;
+                if (P.trace && b == 0 && li == 0 && st.bls_trials - 1 < P.trace_cap) {  // line-search log
+                    float* r = P.trace + (size_t)(st.bls_trials - 1) * kTraceW;
+                    r[0] = (float)outer;
+                    r[1] = (float)inner;
+                    r[2] = (float)trial;
+                    r[3] = lr;
+                    r[4] = f.nl;
+                    r[5] = required;
+                    r[6] = (f.nl > required) ? 0.f : 1.f;
+                    r[7] = loss;
+                    r[8] = gnorm;
+                    r[9] = anorm;
+                }
+                bool inner_end = false, rejected_all = false;
+                float improve = 0.f;
+                if (f.nl > required) {
+                    lr = lr * P.bls_bm;
+                    trial++;
+                    if (trial >= P.max_bls) inner_end = rejected_all = true;  // new_loss = loss
+                } else {
+                    accept = true;
+                    lr = lr * P.bls_bp;
+                    improve = loss - f.nl;
+                    loss = f.nl;
+                    inner_end = true;
+                }
+                if (inner_end) {
+                    if (improve < P.llr) {
+                        to_end = true;
+                    } else {
+                        inner++;
+                        st.inner_iterations++;
+                        snap = true;
+                        if (inner >= P.max_inner) {
+                            to_end = true;
+                        } else if (rejected_all) {
+                            needs_dir = true;  // the same α: X still holds its gradient inputs
+                            bfar = xdense;
+                        } else {
+                            more = true;
+                        }
+                    }
+                }
             }
-            if (lane == 0 && (!done || bfar))
-                atomicOr(&fw[par ^ 1], (done ? 0u : 1u << wave) | (bfar ? 1u << 31 : 0u));
+            if (accept) {
+                // α' = fl(fl(c·α) − fl(lr·ĝ)) (optimizer_GD.py:81, optimizer_BLS.py:139) and its residual
+                // for the next direction (GD: −e/lr folded into stage 2's y''; BLS: e, through dC)
+                const float ne = GD1 ? nilr : -1.f / stepj;
+#pragma unroll
+                for (int j = 0; j < WPL; ++j) {
+                    float G[D];
+                    if constexpr (BLS) {
+#pragma unroll
+                        for (int k = 0; k < D; ++k) G[k] = Gl[j][k];
+                    } else {
+                        grad_alpha(j, e0, e1, G);
+                    }
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        float er;
+                        if constexpr (BLS) {
+                            const float gh = G[k] / gnorm;  // n_alpha_grad (optimizer_BLS.py:165)
+                            al[j][k] = alpha_step(al[j][k], cj, lrj, gh, stepj, G[k], er);
+                        } else {
+                            al[j][k] = alpha_step(al[j][k], cj, stepj, G[k], stepj, G[k], er);
+                        }
+                        q[j][k] = q2[j][k];
+                        v[j][k] = v2[j][k];
+                        if (vl[j]) Eb[(t * D + k) * lde + nn[j]] = BLS ? er : er * ne;
+                    }
+                }
+            }
+            if (snap) snapshot(st);
+            if (to_end) {  // inner loop over: α's exact trajectory and the constraint check next round
+                st.final_loss = loss;
+                phase = LP_RESYNC;
+            }
+            if constexpr (GD1) {
+                if (more) bfar = grad_inputs(w, q2, v2, f.idx, lsg, ljl);
+                if (lane == 0 && (!done || bfar))
+                    atomicOr(&fw[par ^ 1], (done ? 0u : 1u << wave) | (bfar ? 1u << 31 : 0u));
+            } else {
+                if (more) {
+                    bfar = grad_inputs(w, q2, v2, f.idx, lsg, ljl);
+                    xdense = bfar;
+                    needs_dir = true;
+                }
+                if (lane == 0 && phase != LP_DONE)
+                    atomicOr(&fw[par ^ 1], (1u << wave) | (needs_dir ? 1u << 28 : 0u) |
+                                               (phase == LP_RESYNC ? 1u << 29 : 0u) | (bfar ? 1u << 31 : 0u));
+            }
         }
         IRM_STAMP(11);
         __syncthreads();
@@ -1962,31 +2312,36 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_gd_
     }
 
     // ---------------------------------------------------------- epilogue
-    // T = eval_exact(α) (correctly rounded K·α·J), constraintsFulfilled(α) (trajectory.py:129-137,
-    // robot.py:90-113) on it.  Every wave has left the loop after its last barrier: X is free.
-    st.final_loss = loss;
+    if constexpr (GD1) {
+        // T = eval_exact(α) (correctly rounded K·α·J), constraintsFulfilled(α) (trajectory.py:129-137,
+        // robot.py:90-113) on it.  Every wave has left the loop after its last barrier: X is free.
+        st.final_loss = loss;
 #pragma unroll
-    for (int j = 0; j < WPL; ++j) {
-        if (vl[j]) {
+        for (int j = 0; j < WPL; ++j) {
+            if (vl[j]) {
 #pragma unroll
-            for (int k = 0; k < D; ++k) X[nn[j] * kLd + t * D + k] = al[j][k];
+                for (int k = 0; k < D; ++k) X[nn[j] * kLd + t * D + k] = al[j][k];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < WPL; ++j)
+            if (vl[j]) eval_exact<D>(P, X + t * D, nn[j], q[j], v[j]);
+        {
+            WP<D> w[WPL];
+            evaluate(q, v, true, ljl, w);
+        }
+        __syncthreads();
+        if (tvalid) {
+            const Fin f = finalize(lsg);
+            const bool ok = sqrtf(f.a0) < P.eps_p && sqrtf(f.a1) < P.eps_p && sqrtf(f.b0) < P.eps_v &&
+                            sqrtf(f.b1) < P.eps_v && f.tx <= P.pmax && f.tn >= P.pmin && f.va <= P.vmax;
+            st.outer_iterations = 1;
+            st.constraints_ok = ok ? 1 : 0;
         }
     }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < WPL; ++j)
-        if (vl[j]) eval_exact<D>(P, X + t * D, nn[j], q[j], v[j]);
-    {
-        WP<D> w[WPL];
-        evaluate(q, v, true, w);
-    }
-    __syncthreads();
+    // (LF_GD2 / LF_BLS: every trajectory ended through LP_RESYNC — q, v are α's exact trajectory)
     if (tvalid) {
-        const Fin f = finalize();
-        const bool ok = sqrtf(f.a0) < P.eps_p && sqrtf(f.a1) < P.eps_p && sqrtf(f.b0) < P.eps_v &&
-                        sqrtf(f.b1) < P.eps_v && f.tx <= P.pmax && f.tn >= P.pmin && f.va <= P.vmax;
-        st.outer_iterations = 1;
-        st.constraints_ok = ok ? 1 : 0;
 #pragma unroll
         for (int j = 0; j < WPL; ++j) {
             if (vl[j]) {
@@ -2127,12 +2482,26 @@ struct type_tag {
     using type = T;
 };
 
-// LDS of k_gd_single: the optimiser head + obstacles, no staged operator fragments.
+// LDS of k_lean: the optimiser head + obstacles, no staged F fragments, the lean regions.
 inline size_t lean_lds(const KParams& p) {
     KParams q = p;
     q.regops = 1;
-    const int D = p.D;
-    return (size_t)lean_extra(plan_lds(q, false, true).total, p.MP, p.NK, p.RP, p.nsplit, lean_vlds(p.NK, D)).total * 4;
+    return (size_t)lean_extra(plan_lds(q, false, true).total, p.MP, p.NK, p.RP, p.nsplit, lean_vlds(p.NK, p.D),
+                              p.optimizer == IRM_OPT_BLS)
+               .total *
+           4;
+}
+
+// The lean kernel's control flow for a launch (-1: the general kernel serves it): the GD single
+// loop (dualOptimization = max_outer_iteration > 1, optimizer_GD.py:18) without extended-vis
+// snapshots is the bench flow; GD with snapshots or a dual loop, and BLS, the full flows.
+inline int lean_flow(const KParams& p) {
+    if (!p.lean_ok) return -1;
+    if (p.optimizer == IRM_OPT_BLS) return LF_BLS;
+    return (p.max_outer <= 1 && !p.record_series) ? LF_GD1 : LF_GD2;
+}
+inline bool lean_fits(const KParams& p) {
+    return (p.RP / 16) * p.nsplit <= p.BT / 64 && p.NK / 16 <= 4 * p.nsplit && lean_lds(p) <= 160 * 1024;
 }
 
 // k_optimize<Shape> with the MAXT / operator-placement / optimiser variants (one shape per
@@ -2140,29 +2509,35 @@ inline size_t lean_lds(const KParams& p) {
 template <class Sh>
 hipError_t launch_general_shape(const KParams& p, hipStream_t s);
 
+template <class Sh, int TT, int WPL, bool FULL>
+hipError_t launch_lean_flow(const KParams& p, int flow, int grid, hipStream_t s) {
+    switch (flow) {
+        case LF_GD1: return launch_lds(k_lean<Sh, TT, WPL, FULL, LF_GD1>, grid, p.BT, lean_lds(p), s, p);
+        case LF_GD2: return launch_lds(k_lean<Sh, TT, WPL, FULL, LF_GD2>, grid, p.BT, lean_lds(p), s, p);
+        default: return launch_lds(k_lean<Sh, TT, WPL, FULL, LF_BLS>, grid, p.BT, lean_lds(p), s, p);
+    }
+}
+
 template <class Sh>
 hipError_t launch_optimize_shape(const KParams& p, hipStream_t s) {
     const int grid = (p.B + p.TB - 1) / p.TB;
     if (grid <= 0) return hipSuccess;
     return dispatch_t(p.BT, [&](auto tc) {
         constexpr int TT = decltype(tc)::value;
+        const int flow = lean_flow(p);
         if constexpr (!Sh::kVariants && TT == 512) {
             if constexpr (Sh::kNW == 128) {
                 // diagnostic (IRM_LEAN_WPL=2): one wave per trajectory, two waypoints per lane
                 KParams q = p;
                 q.BT = p.BT / 2;
                 q.NW = p.NW / 2;
-                if (p.lean_wpl == 2 && q.lean_ok && q.optimizer == IRM_OPT_GD && q.max_outer <= 1 &&
-                    !q.record_series && (q.RP / 16) * q.nsplit <= q.BT / 64 && q.NK / 16 <= 8 * q.nsplit)
-                    return launch_lds(k_gd_single<Sh, 256, 2>, grid, q.BT, lean_lds(q), s, q);
+                if (p.lean_wpl == 2 && flow == LF_GD1 && lean_fits(q))
+                    return launch_lds(k_lean<Sh, 256, 2>, grid, q.BT, lean_lds(q), s, q);
             }
         }
-        if constexpr (!Sh::kVariants && TT <= 512) {  // GD single loop: the lean kernel
-            // (operators register-resident: one stage-1 unit per wave, enough waves for the units)
-            if (p.lean_ok && p.optimizer == IRM_OPT_GD && p.max_outer <= 1 && !p.record_series &&
-                (p.RP / 16) * p.nsplit <= p.BT / 64 && p.NK / 16 <= 4 * p.nsplit)
-                return p.BT == TT ? launch_lds(k_gd_single<Sh, TT, 1, true>, grid, p.BT, lean_lds(p), s, p)
-                                  : launch_lds(k_gd_single<Sh, TT, 1>, grid, p.BT, lean_lds(p), s, p);
+        if constexpr (!Sh::kVariants && TT <= 512) {  // the lean kernel (F operators register-resident:
+            // one stage-1 unit per wave; workgroups are padded to TT threads by choose_shape)
+            if (flow >= 0 && p.BT == TT && lean_fits(p)) return launch_lean_flow<Sh, TT, 1, true>(p, flow, grid, s);
         }
         if constexpr (!Sh::kVariants && TT == 1024) {
             if constexpr (Sh::kNW == 256 && Sh::D * 3 <= kCols) {  // ≥ 3 trajectories fit the MFMA columns
@@ -2170,9 +2545,8 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s) {
                 KParams q = p;
                 q.BT = p.BT / 2;
                 q.NW = p.NW / 2;
-                if (q.lean_ok && q.optimizer == IRM_OPT_GD && q.max_outer <= 1 && !q.record_series &&
-                    (q.RP / 16) * q.nsplit <= q.BT / 64 && q.NK / 16 <= 4 * q.nsplit)
-                    return launch_lds(k_gd_single<Sh, 512, 2>, grid, q.BT, lean_lds(q), s, q);
+                if (flow >= 0 && flow != LF_BLS && lean_fits(q))
+                    return launch_lean_flow<Sh, 512, 2, false>(q, flow, grid, s);
             }
         }
         return launch_general_shape<Sh>(p, s);

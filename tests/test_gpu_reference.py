@@ -8,7 +8,7 @@ oracle/tools/gen_golden_bench.py from the unmodified reference.
     obstacles), GD single loop in bench mode from the reference's α0: k ≤ 5 steps within
     max(2·spread_k, 1e-3) (SURVEY.md §8c's 1e-3, widened to the reference's own ±1-ulp sensitivity
     after k steps), loss rtol 1e-3; 200 steps within max(2·spread, 3e-3) of the reference's
-    trajectory and the final loss inside the reference ensemble's range ± 1e-3 relative.  k_gd_single
+    trajectory and the final loss inside the reference ensemble's range ± 1e-3 relative.  k_lean
     carries α in fp32 with the reference's rounding (irm_kernels_impl.hpp), which is
     what keeps it inside this band: the same iteration in exact arithmetic ends 1-4e-2 away at C3.
   * BLS line search (optimizer_BLS.py:135-179), the first 4 inner iterations of problem 0 from the

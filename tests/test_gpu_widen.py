@@ -52,10 +52,16 @@ def test_main_cli_batch_mode(tmp_path, capsys):
     assert summ.shape == (B, 6) and np.all(summ[:, 5] == 20)
     s, g = batch_io.batch_problems(B, 3, 3)
     orc = oracle_for(*GD20)
+    from irm_motion_planning_amd.context import Context
+    from irm_motion_planning_amd.params import params_from_args
+    c = Context(params_from_args(ref_args(*GD20)))
     for b in (0, 5, B - 1):
-        t_o, st_o = _oracle_traj(orc, orc.init_alpha(s[b], g[b]), obstacles(), s[b], g[b])
+        # the oracle from the α0 the CLI started from (the device's initTrajectory, bit-equal to
+        # irm_init_alpha; the oracle's own fp32 LU solve of the singular K gives another α0)
+        a0 = c.init_alpha(s[b], g[b])
+        t_o, st_o = _oracle_traj(orc, a0, obstacles(), s[b], g[b])
         assert np.abs(allr[b] - t_o).max() < 2e-3, b
-        assert abs(summ[b, 0] - orc.cost(orc.optimize(orc.init_alpha(s[b], g[b]), obstacles(), s[b], g[b])[0],
+        assert abs(summ[b, 0] - orc.cost(orc.optimize(a0, obstacles(), s[b], g[b])[0],
                                           obstacles(), s[b], g[b], 0, 0, 0)) < 1e-3
 
 

@@ -109,23 +109,27 @@ def test_bench_flop_model():
     exec_f, ref_f = bench.flops_per_iteration(128, 3, 11, 32)
     assert ref_f == 12 * 128 * 128 * 3 + 10 * 128 * 9 + 22 * 128 * 11 == 632320
     assert 0 < exec_f < ref_f
+    assert exec_f == 10 * 32 * 128 * 3 + 8 * 128 * 9 + 42 * 128 * 3 + 14 * 128 * 11 == 167936
 
 
 def test_bench_kernel_label_mirrors_dispatch():
     """bench.py names the optimiser kernel a launch uses (mirrors choose_shape / launch_optimize_shape):
-    the lean GD kernel for the bench-mode BASELINE shapes, the general one for BLS / faithful runs."""
+    the lean kernel for the specialised shapes in every control flow (GD single / dual loop, BLS up to
+    N = 128), the general one for other shapes, ranks and BLS at N = 256."""
     import argparse
 
     import bench
     info = {"traj_per_block": 5, "num_cus": 256, "operator_rank": 32}
     for cfg, want in (("c3", "1 waypoint(s)"), ("c4", "2 waypoint(s)"), ("c5", "1 waypoint(s)"),
-                      ("c7", "1 waypoint(s)"), ("c2", "k_optimize")):
+                      ("c7", "1 waypoint(s)"), ("c2", "BLS dual loop")):
         _, B, N, D, O, opt = bench.CONFIGS[cfg]
         a = argparse.Namespace(tb=0, faithful=False)
         i = dict(info, traj_per_block=16 // D)
         assert want in bench.optimiser_kernel(a, i, N, D, opt, B), cfg
     a = argparse.Namespace(tb=0, faithful=True)
-    assert "k_optimize" in bench.optimiser_kernel(a, info, 128, 3, "gd", 1024)
+    assert "k_lean (GD dual loop" in bench.optimiser_kernel(a, info, 128, 3, "gd", 1024)
+    assert "k_optimize" in bench.optimiser_kernel(a, info, 256, 3, "bls", 1024)
+    assert "k_optimize" in bench.optimiser_kernel(a, info, 100, 3, "gd", 1024)
 
 
 def test_bench_args_bench_mode():

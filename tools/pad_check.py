@@ -1,6 +1,6 @@
 """Diagnostic: bit-equality of the optimiser kernels across workgroup shapes.
 
-For GD single-loop problems, compares the lean kernel (k_gd_single) and the general
+For GD single-loop problems, compares the lean kernel (k_lean) and the general
 kernel (IRM_GENERAL_KERNEL=1) with and without wave padding (IRM_PAD_WAVES) and at a
 fixed trajectories-per-workgroup; prints the fraction of bit-equal trajectories."""
 import os

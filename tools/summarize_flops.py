@@ -1,6 +1,6 @@
 """profiles/<tag>_flops.json from a tools/pmc_flops.sh pass: fp32 flops the optimiser launch issued.
 
-Per dispatch of k_gd_single / k_optimize (mean over dispatches):
+Per dispatch of k_lean / k_optimize (mean over dispatches):
   v_mfma_f32_16x16x4_f32: 16·16·4 MACs = 2048 flops per wave-instruction (SQ_INSTS_MFMA; the kernels
   issue no other MFMA shape);  VALU: 64 lanes × (2 per FMA, 1 per MUL / ADD) per wave-instruction.
 Counts are per issued wave-instruction, so masked-off lanes, padding MFMA columns and the packed
@@ -14,7 +14,7 @@ import os
 import sys
 
 HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("k_gd_single", "k_optimize")
+KERNELS = ("k_lean", "k_optimize")
 
 
 def main():

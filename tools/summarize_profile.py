@@ -21,7 +21,7 @@ def find(d, pattern):
     return hits[0] if hits else None
 
 
-def counter_rows(path, kernel_subs=("k_gd_single", "k_optimize")):
+def counter_rows(path, kernel_subs=("k_lean", "k_optimize")):
     vals = {}
     with open(path) as f:
         for row in csv.DictReader(f):
@@ -39,7 +39,7 @@ def main():
     stats = find(os.path.join(out, "stats"), "*kernel_stats.csv")
     if stats:
         shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    res = {"round": tag, "kernel": "irm::k_gd_single / irm::k_optimize (the optimiser launch)", "command": "python bench.py --no-cpu-baseline --steps 5 --warmup 1"}
+    res = {"round": tag, "kernel": "irm::k_lean / irm::k_optimize (the optimiser launch)", "command": "python bench.py --no-cpu-baseline --steps 5 --warmup 1"}
     for name, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
         path = find(os.path.join(out, sub), "*counter_collection.csv")
         if not path:

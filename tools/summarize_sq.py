@@ -12,7 +12,7 @@ def main():
         per = {}
         with open(path) as f:
             for row in csv.DictReader(f):
-                if "k_optimize" not in row["Kernel_Name"] and "k_gd_single" not in row["Kernel_Name"]:
+                if "k_optimize" not in row["Kernel_Name"] and "k_lean" not in row["Kernel_Name"]:
                     continue
                 key = (row["Dispatch_Id"], row["Counter_Name"])
                 per[key] = per.get(key, 0.0) + float(row["Counter_Value"])
