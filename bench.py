@@ -133,7 +133,7 @@ def optimiser_kernel(a, info, N, D, opt, B):
     wpl = 2 if (nw == 256 and 512 < bt <= 1024) else 1  # N = 256, > 2 trajectories: 2 waypoints/lane
     flow = "BLS dual loop" if opt == "bls" else ("GD dual loop" if a.faithful else "GD single loop")
     lean = ((D, N) in ((3, 50), (3, 64), (3, 128), (3, 256), (7, 128), (7, 256)) and info["operator_rank"] == 32
-            and bt // wpl <= 512 and 2 * nsplit <= waves // wpl and not (opt == "bls" and N > 128))
+            and bt // wpl <= 512 and 2 * nsplit <= waves // wpl)
     return (f"irm::k_lean ({flow}, {wpl} waypoint(s) per lane; fp32 MFMA 16x16x4 + VALU)" if lean
             else "irm::k_optimize (fp32 MFMA 16x16x4 + VALU)")
 

@@ -41,7 +41,7 @@ extern "C" {
 #define IRM_ABI_VERSION 2
 
 #define IRM_MAX_JOINTS 8       /* D  */
-#define IRM_MAX_TIMESTEPS 256  /* N  */
+#define IRM_MAX_TIMESTEPS 512  /* N  */
 #define IRM_MAX_OBSTACLES 64   /* O  */
 #define IRM_MAX_LR 32          /* len(--gd-lr) */
 

@@ -13,7 +13,7 @@ LIB_PATH = os.environ.get("IRM_LIB") or os.path.join(HERE, "libirm_hip.so")
 
 IRM_ABI_VERSION = 2
 IRM_MAX_JOINTS = 8
-IRM_MAX_TIMESTEPS = 256
+IRM_MAX_TIMESTEPS = 512
 IRM_MAX_OBSTACLES = 64
 IRM_MAX_LR = 32
 

@@ -159,7 +159,10 @@ enum ColdWord : int {
     C_JINV = 128,   // J⁻¹, D×D
     kColdWords = 192
 };
-__host__ __device__ constexpr Head plan_head(int MP, int RP, int nsplit, bool optimizer) {
+// lean: the layout of k_lean (stage-1 partials [split][column][r], stride RP + 8) instead of
+// k_optimize's [split][r][column] (stride kLd) — 640 instead of 544 floats per split at RP = 32,
+// which decides whether N = 512 fits the general kernel's 160 KiB.
+__host__ __device__ constexpr Head plan_head(int MP, int RP, int nsplit, bool optimizer, bool lean = false) {
     Head H{};
     H.X = 0;
     H.dP = H.X + al4(MP * kLd);
@@ -167,7 +170,7 @@ __host__ __device__ constexpr Head plan_head(int MP, int RP, int nsplit, bool op
     H.Ypart = H.Ymix = 0;
     if (optimizer) {
         H.Ypart = off;
-        off += al4(nsplit * (RP * kLd > 16 * (RP + 8) ? RP * kLd : 16 * (RP + 8)));
+        off += al4(nsplit * (lean ? 16 * (RP + 8) : RP * kLd));
         H.Ymix = off;
         off += al4(RP * kLd);
     }
@@ -188,8 +191,8 @@ __host__ __device__ constexpr Head plan_head(int MP, int RP, int nsplit, bool op
     return H;
 }
 
-__host__ __device__ inline Plan plan_lds(const KParams& p, bool ops_lds, bool optimizer) {
-    const Head H = plan_head(p.MP, p.RP, p.nsplit, optimizer);
+__host__ __device__ inline Plan plan_lds(const KParams& p, bool ops_lds, bool optimizer, bool lean = false) {
+    const Head H = plan_head(p.MP, p.RP, p.nsplit, optimizer, lean);
     Plan L{};
     L.X = H.X;
     L.Bs = L.X + p.NK * kLd;
@@ -219,13 +222,11 @@ __host__ __device__ inline Plan plan_lds(const KParams& p, bool ops_lds, bool op
 // endpoint operator columns hL (2·MP), G's endpoint columns hV (2·NK), the V_R fragments (when
 // staged: vlds), the rounding residual rows e' ([column][waypoint], stride NK + 8), its stage-1
 // partials zp ([split][column][r], stride RP + 8) and the gradient rows G ([column][waypoint]).
-// With the BLS flow also dc: F·(V_Rᵀ·e) [column][row] (stride MP + 8), the rounding residual's
-// waypoint-space correction (the line search's trial steps cannot carry it folded into y'').
 struct LeanX {
-    int hl, hv, vt, vn, eb, zp, gb, dc, total;
+    int hl, hv, vt, vn, eb, zp, gb, total;
 };
 __host__ __device__ constexpr int lean_ld(int NK) { return NK + 8; }
-__host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, int nsplit, bool vlds, bool bls = false) {
+__host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, int nsplit, bool vlds) {
     LeanX e{};
     int off = base;
     e.hl = off;
@@ -245,11 +246,6 @@ __host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, in
     off += al4(nsplit * 16 * (RP + 8));
     e.gb = off;
     off += al4(16 * lean_ld(NK));
-    e.dc = 0;
-    if (bls) {
-        e.dc = off;
-        off += al4(16 * (MP + 8));
-    }
     e.total = off;
     return e;
 }

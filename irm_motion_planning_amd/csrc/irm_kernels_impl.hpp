@@ -480,8 +480,30 @@ __device__ void eval_exact(const KParams& P, const float* __restrict__ Xa, int n
     for (int d = 0; d < D; ++d) aq[d] = av[d] = 0.0;
     const float* kt = (Kt ? Kt : P.Kt) + n;
     const float* dkt = (dKt ? dKt : P.dKt) + n;
-    for (int m = 0; m < N; ++m) {
-        const double kq = (double)kt[(size_t)m * N], kv = (double)dkt[(size_t)m * N];  // K[n][m], dK[n][m]
+    // K / dK rows come from L2 / HBM: 8 rows in flight per batch (the sum stays in the sequential
+    // order m = 0, 1, …, N−1 of the oracle)
+    constexpr int U = 8;
+    int m0 = 0;
+    for (; m0 + U <= N; m0 += U) {
+        float kq[U], kv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            kq[u] = kt[(size_t)(m0 + u) * N];  // K[n][m]
+            kv[u] = dkt[(size_t)(m0 + u) * N]; // dK[n][m]
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float* xr = Xa + (m0 + u) * rs;
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const double x = (double)xr[d * cs];
+                aq[d] = fma((double)kq[u], x, aq[d]);
+                av[d] = fma((double)kv[u], x, av[d]);
+            }
+        }
+    }
+    for (int m = m0; m < N; ++m) {
+        const double kq = (double)kt[(size_t)m * N], kv = (double)dkt[(size_t)m * N];
         const float* xr = Xa + m * rs;
 #pragma unroll
         for (int d = 0; d < D; ++d) {
@@ -1497,7 +1519,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     static_assert(NWL % 64 == 0, "whole waves per trajectory");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const S sh(P);
-    const Head H = plan_head(sh.MP, sh.RP, sh.NSPLIT, true);
+    const Head H = plan_head(sh.MP, sh.RP, sh.NSPLIT, true, true);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nwaves = FULL ? MAXT / 64 : P.BT >> 6;
@@ -1530,13 +1552,12 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     unsigned* fw = reinterpret_cast<unsigned*>(smem + H.flags);
     float* obsL = smem + H.obs;
     const int nsplit = sh.NSPLIT;
-    const LeanX LX = lean_extra(plan_lds(P, false, true).total, MP, NK, RP, nsplit, VL, BLS);
+    const LeanX LX = lean_extra(plan_lds(P, false, true, true).total, MP, NK, RP, nsplit, VL);
     float* hL = smem + LX.hl;  // endpoint columns of F·Fᵀ (2·MP), read per round when WPL > 1
     float* hVL = smem + LX.hv; // G's endpoint columns (2·NK), read per round when WPL > 1
     float* Eb = smem + LX.eb;  // e' rows [column][waypoint]
     float* Zp = smem + LX.zp;  // stage-1 partials of V_Rᵀ·e'
     float* Gb = smem + LX.gb;  // (V_R·y'')[waypoint] rows [column][waypoint]
-    float* dC = smem + LX.dc;  // BLS: F·(V_Rᵀ·e) rows [column][row]
     const float* VT = VL ? smem + LX.vt : P.VTp;
     const float* VN = VL ? smem + LX.vn : P.VNp;
 
@@ -1812,15 +1833,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             *reinterpret_cast<f32x4*>(Zp + (sp * 16 + cl) * ldy + tile * 16 + r4) = acc0 + acc1;
         }
     };
-    // stage 2: dP = F·(Σ_s Ypart[s] (+ Σ_s Zp[s]: GD, the folded residual)), Gb = V_R·Σ_s Ypart[s];
-    // BLS: dC = F·Σ_s Zp[s] separately
+    // stage 2: dP = F·(Σ_s Ypart[s] + Σ_s Zp[s]) (the pending residual folded in), Gb = V_R·Σ_s Ypart[s]
     auto stage2 = [&]() {
-        f32x4 acc[S2T], acz[BLS ? S2T : 1];
+        f32x4 acc[S2T];
 #pragma unroll
-        for (int j = 0; j < S2T; ++j) {
-            acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if constexpr (BLS) acz[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
+        for (int j = 0; j < S2T; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
         f32x4 by[2], bt[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -1831,7 +1848,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     by[i] += *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + cl) * ldy + i * 16 + r4);
                     bz += *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + i * 16 + r4);
                 }
-                bt[i] = BLS ? bz : by[i] + bz;
+                bt[i] = by[i] + bz;
             }
         }
 #pragma unroll
@@ -1840,25 +1857,17 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
                 for (int j = 0; j < S2T; ++j) {
                     if (wave + j * nwaves < MT2) {
-                        const f32x4 bd = BLS ? by[i] : bt[i];
 #pragma unroll
                         for (int m = 0; m < 4; ++m)
-                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][m], bd[m], acc[j], 0, 0, 0);
-                        if constexpr (BLS) {
-#pragma unroll
-                            for (int m = 0; m < 4; ++m)
-                                acz[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][m], bt[i][m], acz[j], 0, 0, 0);
-                        }
+                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][m], bt[i][m], acc[j], 0, 0, 0);
                     }
                 }
             }
         }
 #pragma unroll
         for (int j = 0; j < S2T; ++j) {
-            if (wave + j * nwaves < MT2) {
+            if (wave + j * nwaves < MT2)
                 *reinterpret_cast<f32x4*>(dP + cl * ldx + (wave + j * nwaves) * 16 + r4) = acc[j];
-                if constexpr (BLS) *reinterpret_cast<f32x4*>(dC + cl * ldx + (wave + j * nwaves) * 16 + r4) = acz[j];
-            }
         }
         // G tiles (waypoint rows of V_R·y''), from the top wave down
         for (int u = nwaves - 1 - wave; u < MTG; u += nwaves) {
@@ -1967,10 +1976,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     IRM_STAMP(14);
     // ---------------------------------------------------------- rounds
     float dTl[BLS ? WPL : 1][D], dVl[BLS ? WPL : 1][D], Gl[BLS ? WPL : 1][D];  // BLS: latched direction
+    // BLS: the rounding residual not yet in [T; V] (α units) and the reference step it is folded into
+    // y'' with (e' = −pend/sref): trial j applies the fraction s_j/sref of it, the rest carries over
+    float pend[BLS ? WPL : 1][D], sref = 1.f;
 #pragma unroll
     for (int j = 0; j < (BLS ? WPL : 1); ++j)
 #pragma unroll
-        for (int k = 0; k < D; ++k) dTl[j][k] = dVl[j][k] = Gl[j][k] = 0.f;
+        for (int k = 0; k < D; ++k) dTl[j][k] = dVl[j][k] = Gl[j][k] = pend[j][k] = 0.f;
     for (int par = 0;; par ^= 1) {
         const unsigned fl = fw[par];
         if constexpr (GD1) {
@@ -2033,27 +2045,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             if (needs_dir) {  // wave-uniform; the inner-loop head (optimizer_BLS.py:163-166)
 #pragma unroll
                 for (int j = 0; j < WPL; ++j) {
-                    direction(j, e0, e1, dTl[j], dVl[j]);
+                    direction(j, e0, e1, dTl[j], dVl[j]);  // includes the folded residual −pend/sref
                     grad_alpha(j, e0, e1, Gl[j]);
-                    // the pending rounding residual of the last accepted trial: [T; V] += L·e·J
-                    float ct[D], cv[D];
-#pragma unroll
-                    for (int k = 0; k < D; ++k) {
-                        ct[k] = dC[(t * D + k) * ldx + nn[j]];
-                        cv[k] = dC[(t * D + k) * ldx + NK + nn[j]];
-                    }
-#pragma unroll
-                    for (int k = 0; k < D; ++k) {
-                        float a = 0.f, c = 0.f;
-#pragma unroll
-                        for (int l = 0; l < D; ++l) {
-                            a = fmaf(ct[l], P.J[l * D + k], a);
-                            c = fmaf(cv[l], P.J[l * D + k], c);
-                        }
-                        q[j][k] += a;
-                        v[j][k] += c;
-                        if (vl[j]) Eb[(t * D + k) * lde + nn[j]] = 0.f;  // consumed
-                    }
                 }
                 gnorm = sqrtf(wp[t * 2]);
                 anorm = wp[t * 2 + 1] / gnorm;
@@ -2075,6 +2068,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                             X[(t * D + k) * ldx + nn[j]] = al[j][k];
                             Eb[(t * D + k) * lde + nn[j]] = 0.f;  // absorbed by the exact trajectory
                         }
+                    }
+                    if constexpr (BLS) {
+#pragma unroll
+                        for (int k = 0; k < D; ++k) pend[j][k] = 0.f;
                     }
                 }
             }
@@ -2252,6 +2249,12 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                         } else if (rejected_all) {
                             needs_dir = true;  // the same α: X still holds its gradient inputs
                             bfar = xdense;
+                            sref = lr / gnorm;  // refold the pending residual for the next trial series
+#pragma unroll
+                            for (int j = 0; j < WPL; ++j)
+                                if (vl[j])
+#pragma unroll
+                                    for (int k = 0; k < D; ++k) Eb[(t * D + k) * lde + nn[j]] = -pend[j][k] / sref;
                         } else {
                             more = true;
                         }
@@ -2262,6 +2265,14 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 // α' = fl(fl(c·α) − fl(lr·ĝ)) (optimizer_GD.py:81, optimizer_BLS.py:139) and its residual
                 // for the next direction (GD: −e/lr folded into stage 2's y''; BLS: e, through dC)
                 const float ne = GD1 ? nilr : -1.f / stepj;
+                // BLS: [T; V] took the fraction s_j/sref of the pending residual; the rest (scaled by
+                // c_j like α) stays pending with this trial's residual, refolded for the next direction
+                float keep = 0.f, nsr = 0.f;
+                if constexpr (BLS) {
+                    keep = cj - stepj / sref;
+                    sref = lr / gnorm;  // the next trial 0's step (lr already ·β+): keep ≈ 0 there
+                    nsr = -1.f / sref;
+                }
 #pragma unroll
                 for (int j = 0; j < WPL; ++j) {
                     float G[D];
@@ -2282,7 +2293,12 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                         }
                         q[j][k] = q2[j][k];
                         v[j][k] = v2[j][k];
-                        if (vl[j]) Eb[(t * D + k) * lde + nn[j]] = BLS ? er : er * ne;
+                        if constexpr (BLS) {
+                            pend[j][k] = er + keep * pend[j][k];
+                            if (vl[j]) Eb[(t * D + k) * lde + nn[j]] = nsr * pend[j][k];
+                        } else {
+                            if (vl[j]) Eb[(t * D + k) * lde + nn[j]] = er * ne;
+                        }
                     }
                 }
             }
@@ -2486,10 +2502,7 @@ struct type_tag {
 inline size_t lean_lds(const KParams& p) {
     KParams q = p;
     q.regops = 1;
-    return (size_t)lean_extra(plan_lds(q, false, true).total, p.MP, p.NK, p.RP, p.nsplit, lean_vlds(p.NK, p.D),
-                              p.optimizer == IRM_OPT_BLS)
-               .total *
-           4;
+    return (size_t)lean_extra(plan_lds(q, false, true, true).total, p.MP, p.NK, p.RP, p.nsplit, lean_vlds(p.NK, p.D)).total * 4;
 }
 
 // The lean kernel's control flow for a launch (-1: the general kernel serves it): the GD single
@@ -2545,8 +2558,7 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s) {
                 KParams q = p;
                 q.BT = p.BT / 2;
                 q.NW = p.NW / 2;
-                if (flow >= 0 && flow != LF_BLS && lean_fits(q))
-                    return launch_lean_flow<Sh, 512, 2, false>(q, flow, grid, s);
+                if (flow >= 0 && lean_fits(q)) return launch_lean_flow<Sh, 512, 2, false>(q, flow, grid, s);
             }
         }
         return launch_general_shape<Sh>(p, s);

@@ -20,6 +20,9 @@ the jax API; eager jit / while_loop / cond) and commits only generated arrays:
                                   the GD λ_max table at N=50, GD at N=128 / 256, BLS at N=256 (C4
                                   obstacles), each with a ±1-ulp ensemble (avg / max cost, flag,
                                   gradient-call count)
+  tests/golden/ref_e2e_n500.npz   the same for GD and BLS at N=500 (--only n500), with the reference's
+                                  α0 (its fp32 LU solve differs from any other at this size: the runs
+                                  under test start from it)
 
     PYTHONDONTWRITEBYTECODE=1 python oracle/tools/gen_golden_bench.py [--only c3,c4,bls,e2e]
     PYTHONDONTWRITEBYTECODE=1 python oracle/tools/gen_golden_bench.py --matmul exact --only c3,c4,bls,e2e,e2e1
@@ -203,11 +206,11 @@ def main():
                 for k, v in bls_trial_fixture(refmain, obls, trajmod, N, kind, 4).items():
                     bl[f"n{N}_{kind}__{k}"] = v
         np.savez_compressed(os.path.join(OUT, f"ref_bls_trials{sfx}.npz"), **bl)
-    if "e2e" in only or "e2e1" in only:
+    if "e2e" in only or "e2e1" in only or "n500" in only:
         import bench
         cnt = gg.CallCounter(trajmod)
 
-        def record(e2e, tag, mod, cls, args, obstacles=None, ensemble=8):
+        def record(e2e, tag, mod, cls, args, obstacles=None, ensemble=8, store_alpha0=False):
             o = gg.make_opt(mod, cls, args, obstacles)
             r = gg.end_to_end(o, cnt)
             for k, v in r.items():
@@ -216,6 +219,8 @@ def main():
             tr, env = o.trajectory, o.env
             init = tr.initTrajectory
             a0 = np.array(init(env.start_config, env.goal_config), np.float32)
+            if store_alpha0:  # the reference's initTrajectory (its fp32 LU solve of the singular K)
+                e2e[f"{tag}__alpha0"] = a0
             ens = {"avg_cost": [], "max_cost": [], "constraints_ok": [], "grad_calls": []}
             for seed in range(ensemble):
                 tr.initTrajectory = lambda s_, g_, a=perturb(a0, seed): a.copy()
@@ -242,6 +247,13 @@ def main():
             record(e2e, "bls_n256_c4obs", obls, "BacktrackingLineSearchOptimizer",
                    gg.ref_args(refmain, n_timesteps=256), obstacles=obs_c4, ensemble=6)
             np.savez_compressed(os.path.join(OUT, f"ref_e2e_r02{sfx}.npz"), **e2e)
+        if "n500" in only:  # N > 256 (the blog's runtime study goes to N = 500): reference defaults
+            e2e = {}
+            record(e2e, "gd_n500", ogd, "GradientDescentOptimizer",
+                   gg.ref_args(refmain, n_timesteps=500, optimizer_name="gd"), ensemble=4, store_alpha0=True)
+            record(e2e, "bls_n500", obls, "BacktrackingLineSearchOptimizer",
+                   gg.ref_args(refmain, n_timesteps=500), ensemble=4, store_alpha0=True)
+            np.savez_compressed(os.path.join(OUT, f"ref_e2e_n500{sfx}.npz"), **e2e)
         if "e2e1" in only:  # gen_golden.py's end-to-end cases (ref_e2e.npz), here with exact matmuls
             assert sfx, "the BLAS variant of these cases is gen_golden.py's ref_e2e.npz"
             e2e = {}

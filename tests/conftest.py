@@ -100,7 +100,8 @@ def e2e_reference(tag):
     reference's fp32 BLAS matmuls (ref_e2e*.npz) and with correctly rounded matmuls (*_xm.npz, the
     contraction arithmetic of this build; oracle/tools/gen_golden_bench.py --matmul exact)."""
     out = {}
-    for variant, names in (("blas", ("ref_e2e", "ref_e2e_r02")), ("xm", ("ref_e2e_xm", "ref_e2e_r02_xm"))):
+    for variant, names in (("blas", ("ref_e2e", "ref_e2e_r02", "ref_e2e_n500")),
+                           ("xm", ("ref_e2e_xm", "ref_e2e_r02_xm", "ref_e2e_n500_xm"))):
         for name in names:
             g = _golden_cached(name)
             if f"{tag}__avg_cost" in g:

@@ -118,7 +118,7 @@ def _create(p):
 
 @pytest.mark.parametrize("field,value,msg", [
     ("n_timesteps", 1, "n_timesteps"),
-    ("n_timesteps", 257, "n_timesteps"),
+    ("n_timesteps", 513, "n_timesteps"),
     ("n_joints", 9, "n_joints"),
     ("optimizer", 7, "optimizer"),
     ("rbf_variance", 0.0, "rbf_variance"),

@@ -22,7 +22,8 @@ import numpy as np
 import pytest
 
 from conftest import GOAL, START, check_iterations, check_quality, golden, params
-from test_reference_bench import BENCH_ARGS, BLS_CASES, BLS_LOG_ARGS, E2E_R02, bench_band, check_bls_log, e2e_obstacles
+from test_reference_bench import (BENCH_ARGS, BLS_CASES, BLS_LOG_ARGS, E2E_R02, bench_band, check_bls_log, e2e_alpha0,
+                                  e2e_obstacles)
 
 pytestmark = pytest.mark.gpu
 
@@ -115,7 +116,7 @@ def test_end_to_end_r02(tag):
     argv, src = E2E_R02[tag]
     c = ctx(*argv)
     obs = e2e_obstacles(src)
-    alpha, _, st = c.optimize(START, GOAL, obs)
+    alpha, _, st = c.optimize(START, GOAL, obs, alpha0=e2e_alpha0(tag))
     avg = float(c.eval_cost(alpha, obs, START, GOAL, 0, 0, 0))
     mx = float(c.eval_cost(alpha, obs, START, GOAL, 0, 0, 1))
     ok, rep = c.constraints(alpha, START, GOAL)

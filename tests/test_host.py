@@ -128,7 +128,7 @@ def test_bench_kernel_label_mirrors_dispatch():
         assert want in bench.optimiser_kernel(a, i, N, D, opt, B), cfg
     a = argparse.Namespace(tb=0, faithful=True)
     assert "k_lean (GD dual loop" in bench.optimiser_kernel(a, info, 128, 3, "gd", 1024)
-    assert "k_optimize" in bench.optimiser_kernel(a, info, 256, 3, "bls", 1024)
+    assert "k_lean (BLS dual loop, 2 waypoint" in bench.optimiser_kernel(a, info, 256, 3, "bls", 1024)
     assert "k_optimize" in bench.optimiser_kernel(a, info, 100, 3, "gd", 1024)
 
 
