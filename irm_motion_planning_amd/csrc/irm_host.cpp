@@ -245,7 +245,7 @@ struct irm_ctx {
     // device
     float *d_K = nullptr, *d_dK = nullptr, *d_Kt = nullptr, *d_dKt = nullptr, *d_F1 = nullptr, *d_F2 = nullptr,
           *d_F1p = nullptr, *d_F2p = nullptr, *d_Fbot = nullptr, *d_Vr = nullptr, *d_H = nullptr, *d_u = nullptr, *d_w = nullptr,
-          *d_VTp = nullptr, *d_VNp = nullptr, *d_HV = nullptr;
+          *d_VTp = nullptr, *d_VNp = nullptr, *d_HV = nullptr, *d_VTs = nullptr, *d_VNs = nullptr;
     // host-API staging
     void* d_io = nullptr;
     size_t io_bytes = 0;
@@ -591,11 +591,15 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
             for (int r = 0; r < RP; ++r) A[(size_t)r * NK + n] = Vd[(size_t)n * RP + r];
         fill_frag(frag, RP, NK, A, true);
         rc |= upload(&c->d_VTp, frag);
+        fill_frag(frag, RP, NK, A);
+        rc |= upload(&c->d_VTs, frag);
         A.assign((size_t)NK * RP, 0.0);
         for (int n = 0; n < N; ++n)
             for (int r = 0; r < RP; ++r) A[(size_t)n * RP + r] = Vd[(size_t)n * RP + r];
         fill_frag(frag, NK, RP, A, true);
         rc |= upload(&c->d_VNp, frag);
+        fill_frag(frag, NK, RP, A);
+        rc |= upload(&c->d_VNs, frag);
         std::vector<float> hv((size_t)2 * NK, 0.f);
         for (int e = 0; e < 2; ++e) {
             const int me = N + (e ? N - 1 : 0);
@@ -767,6 +771,8 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
     kp.VTp = c->d_VTp;
     kp.VNp = c->d_VNp;
     kp.HV = c->d_HV;
+    kp.VTs = c->d_VTs;
+    kp.VNs = c->d_VNs;
     kp.uvec = c->d_u;
     kp.wvec = c->d_w;
     kp.lam_max = p->lambda_max_cost;
@@ -804,7 +810,7 @@ void irm_ctx_destroy(irm_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->p.device);
     float* bufs[] = {c->d_K, c->d_dK, c->d_Kt, c->d_dKt, c->d_F1,   c->d_F2, c->d_F1p, c->d_F2p,
-                     c->d_Fbot, c->d_Vr, c->d_H, c->d_u, c->d_w, c->d_VTp, c->d_VNp, c->d_HV};
+                     c->d_Fbot, c->d_Vr, c->d_H, c->d_u, c->d_w, c->d_VTp, c->d_VNp, c->d_HV, c->d_VTs, c->d_VNs};
     for (float* b : bufs)
         if (b) (void)hipFree(b);
     if (c->d_io) (void)hipFree(c->d_io);

@@ -72,6 +72,8 @@ struct KParams {
     const float* VTp;     // V_Rᵀ (RP × NK): z = V_Rᵀ·e' (the rounding residual of α into waypoint space)
     const float* VNp;     // V_R (NK × RP):  G = V_R·y'·J⁻¹ (the α-space gradient, per waypoint)
     const float* HV;      // V_R·F[NK]ᵀ, V_R·F[NK+N−1]ᵀ: G's endpoint velocity columns (2 × NK)
+    const float* VTs;     // V_Rᵀ / V_R in the standard fragment layout (frag_index) of the general
+    const float* VNs;     //   kernel's GD rounding terms
     const float* uvec;    // K⁻¹(1-c)   (N)  initTrajectory basis
     const float* wvec;    // K⁻¹c       (N)
     // batch I/O
@@ -157,7 +159,8 @@ enum ColdWord : int {
     C_MINV = 56,    // (JᵀJ)⁻¹, D×D
     C_WAL = 120,    // D
     C_JINV = 128,   // J⁻¹, D×D
-    kColdWords = 192
+    C_J = 192,      // J, D×D
+    kColdWords = 256
 };
 // lean: the layout of k_lean (stage-1 partials [split][column][r], stride RP + 8) instead of
 // k_optimize's [split][r][column] (stride kLd) — 640 instead of 544 floats per split at RP = 32,

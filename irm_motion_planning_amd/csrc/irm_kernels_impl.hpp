@@ -614,6 +614,31 @@ __device__ __forceinline__ void ered_store(bool live, float cv, float us, float 
     }
 }
 
+// A value the compiler may not fuse into a neighbouring operation (hipcc contracts a·b − c into
+// an fma even under `#pragma clang fp contract(off)` when the product comes from __fmul_rn).
+__device__ __forceinline__ float unfused(float x) {
+    asm("" : "+v"(x));
+    return x;
+}
+
+// One fp32 α element of the reference's GD / BLS update and its rounding residual:
+//   α' = fl(fl(c·α) − fl(lr·ĝ))                        (optimizer_GD.py:81, optimizer_BLS.py:139)
+//   e  = α' − (c·α − step·G)  exactly (to fp32 rounding of e itself), where c·[T; V] − step·F·y'
+//        is the waypoint-space update the kernel applies (ĝ = G for GD, G/‖G‖ for BLS).
+// Products and the subtraction are rounded separately (the reference's arithmetic, no fma); the
+// residuals come from fma (c·α − fl(c·α) is exact) and TwoSum.
+__device__ __forceinline__ float alpha_step(float al, float c, float lr, float gh, float step, float G, float& e) {
+    const float p1 = unfused(c * al), p2 = unfused(lr * gh);
+    const float an = unfused(p1 - p2);
+    const float ep1 = fmaf(c, al, -p1);                 // c·α − p1
+    const float bb = an - p1;                           // TwoSum(p1, −p2) = an + es
+    const float es = (p1 - (an - bb)) + (-p2 - bb);
+    const float p = unfused(step * G);
+    const float ep = fmaf(step, G, -p);                 // step·G − p
+    e = (((p - p2) - es) + ep) - ep1;                   // α' − (c·α − step·G)
+    return an;
+}
+
 // Operator fragments a wave keeps in VGPRs across all rounds (REGOPS).
 // Capacities mirror regops_fit (irm_kernels.hpp): a 512-thread workgroup (8 waves) keeps 4 stage-1
 // k-quads and 2 stage-2 tiles per wave (N ≤ 128 at R = 32), a 256-thread one up to 8 of each.
@@ -766,6 +791,12 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
     const float fb1 = yrow ? P.Fbot[(size_t)(N - 1) * RP + n] : 0.f;
     stage_obstacles(P, tb0, ntb, obsL);
     for (int e = tid; e < RP * kLd; e += P.BT) Ymix[e] = 0.f;
+    // GD: the rounding residual rows e' live in dP's direction columns between an accepted step and
+    // the next stage 1 (stage 2 rewrites dP only after the stage-1 barrier); none pending at start
+    if constexpr (!BLS)
+        for (int e = tid; e < MP * kLd; e += P.BT) dP[e] = 0.f;
+    // GD: G's endpoint velocity columns for this lane's row (G = V_R·y'·J⁻¹, see the latch)
+    const float hv0 = (!BLS && valid) ? P.HV[n] : 0.f, hv1 = (!BLS && valid) ? P.HV[NK + n] : 0.f;
     if (tid < 8) flagw[tid] = 0u;
     // Parameters used only on rare paths (outer-loop step, line search, resync, series) live in
     // LDS so that they hold no SGPRs across the loop.
@@ -795,6 +826,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
         } else if (i >= C_MINV && i < C_MINV + D * D) val = P.Minv[i - C_MINV];
         else if (i >= C_WAL && i < C_WAL + D) val = P.wal[i - C_WAL];
         else if (i >= C_JINV && i < C_JINV + D * D) val = P.Jinv[i - C_JINV];
+        else if (i >= C_J && i < C_J + D * D) val = P.J[i - C_J];
         cold[i] = val;
     }
     auto cold_ptr = [&](int w) -> float* {
@@ -807,11 +839,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
     // T0 = (K·α0)·J, V0 = (dK·α0)·J  (trajectory.py:63-65), correctly rounded.
     // ab: this lane's row of the α the state is expressed against (α0, then the α
     // materialised at the last resync).
-    float q[D], v[D], s[D], g[D], ab[D], dT[D], dV[D], dra[D], drb[D], aca[D], acb[D];
+    float q[D], v[D], s[D], g[D], ab[D], dT[D], dV[D], dra[D], drb[D], aca[D], acb[D], Gl[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) {
         q[k] = v[k] = 0.f;
-        dT[k] = dV[k] = dra[k] = drb[k] = aca[k] = acb[k] = 0.f;
+        dT[k] = dV[k] = dra[k] = drb[k] = aca[k] = acb[k] = Gl[k] = 0.f;
         ab[k] = valid ? X[n * kLd + t * D + k] : 0.f;
         s[k] = tvalid ? P.start[b * D + k] : 0.f;
         g[k] = tvalid ? P.goal[b * D + k] : 0.f;
@@ -952,6 +984,25 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
             IRM_STAMP(1);
             IRM_COUNT(13, dense);
             stage1(dense);
+            if constexpr (!BLS) {
+                // GD: z = V_Rᵀ·e' (the last accepted step's rounding residual, e' = −e·J/lr, rows of dP)
+                // into Ymix, one unit per r-tile over all k-quads, operator from L2 — added to y' for
+                // stage 2's F tiles, i.e. [T; V] += L·e·J one step late (k_lean's scheme)
+                const float* xl = dP + (lane >> 4) * kLd + (lane & 15);
+                for (int u = nwaves - 1 - wave; u < MT1; u += nwaves) {
+                    const f32x4* ap = reinterpret_cast<const f32x4*>(P.VTs) + (size_t)u * KQa * 64 + lane;
+                    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+                    for (int kq = 0; kq < KQa; ++kq) {
+                        const f32x4 a = ap[(size_t)kq * 64];
+                        const float* xb = xl + kq * 16 * kLd;
+                        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], xb[0], acc0, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], xb[4 * kLd], acc1, 0, 0, 0);
+                        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], xb[8 * kLd], acc0, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], xb[12 * kLd], acc1, 0, 0, 0);
+                    }
+                    store_tile(Ymix, u, acc0 + acc1, 0xFFFFu);
+                }
+            }
             IRM_STAMP(5);
             __syncthreads();
             IRM_STAMP(0);
@@ -988,7 +1039,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
             // stage 2: dP = F(MP × RP)·Σ_s Ypart[s], only the direction columns
             {
                 const float* xl = Ypart + (lane >> 4) * kLd + (lane & 15);
-                auto bload = [&](int i, float& b0, float& b1, float& b2, float& b3) {
+                // y' rows (+ GD: z, the folded rounding residual, for the F tiles)
+                auto bload = [&](int i, float& b0, float& b1, float& b2, float& b3, bool withz = !BLS) {
                     b0 = b1 = b2 = b3 = 0.f;
                     for (int sp = 0; sp < nsplit; ++sp) {
                         const float* xb = xl + (sp * RP + i * 16) * kLd;
@@ -997,7 +1049,32 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                         b2 += xb[8 * kLd];
                         b3 += xb[12 * kLd];
                     }
+                    if (withz) {
+                        const float* zb = Ymix + (i * 16 + (lane >> 4)) * kLd + (lane & 15);
+                        b0 += zb[0];
+                        b1 += zb[4 * kLd];
+                        b2 += zb[8 * kLd];
+                        b3 += zb[12 * kLd];
+                    }
                 };
+                if constexpr (!BLS) {
+                    // G tiles: (V_R·y')[waypoint] into X's position rows (X was consumed by stage 1;
+                    // only the direction columns are written), from the top wave down
+                    for (int u = nwaves - 1 - wave; u < KQa; u += nwaves) {
+                        const f32x4* ap = reinterpret_cast<const f32x4*>(P.VNs) + (size_t)u * KQ2 * 64 + lane;
+                        f32x4 c0 = {0.f, 0.f, 0.f, 0.f};
+                        for (int i = 0; i < KQ2; ++i) {
+                            float b0, b1, b2, b3;
+                            bload(i, b0, b1, b2, b3, false);
+                            const f32x4 a = ap[(size_t)i * 64];
+                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b0, c0, 0, 0, 0);
+                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b1, c0, 0, 0, 0);
+                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b2, c0, 0, 0, 0);
+                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b3, c0, 0, 0, 0);
+                        }
+                        store_tile(X, u, c0, dirmask);
+                    }
+                }
                 if (REGOPS) {
                     f32x4 acc[S2T];
 #pragma unroll
@@ -1071,8 +1148,20 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                     phase = PH_BLS_TRIAL;
                     trial = 0;
                 } else {
-                    cfac = 1.f - P.lreg * lr;
+                    cfac = P.gd_c[outer];  // fp32(1 − λ_reg·lr) from the Python doubles (optimizer_GD.py:185)
                     step = lr;
+                    // G = (V_R·y')·J⁻¹ + its endpoint velocity columns (y' = y·JᵀJ, G = V_R·y·Jᵀ)
+                    float gr[D];
+#pragma unroll
+                    for (int k = 0; k < D; ++k)
+                        gr[k] = valid ? fmaf(hv0, e0[k], fmaf(hv1, e1[k], X[n * kLd + t * D + k])) : 0.f;
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        float gk = 0.f;
+#pragma unroll
+                        for (int l = 0; l < D; ++l) gk = fmaf(gr[l], cold[C_JINV + l * D + k], gk);
+                        Gl[k] = gk;
+                    }
                 }
                 needs_dir = false;
             }
@@ -1086,7 +1175,27 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
         // V_R·(Fᵀ·acc)·J⁻¹ in fp32 (what the reference carries), then [T; V] =
         // eval_exact(α), so the constraint check below and the caller's
         // evaluate(α_out) see the same waypoints bit for bit.
-        if (rmask) {  // block-uniform
+        if (rmask && !BLS) {  // block-uniform; GD: α is carried explicitly
+            const bool rs = tvalid && ((rmask >> t) & 1u);  // wave-uniform
+            if (rs && valid) {
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    X[n * kLd + t * D + k] = ab[k];
+                    dP[n * kLd + t * D + k] = 0.f;  // the pending residual is in the exact trajectory
+                }
+            }
+            __syncthreads();
+            if (rs && valid) {
+                eval_exact<D>(P, X + t * D, n, q, v, cold_ptr(2), cold_ptr(3));
+                if (rec && st.series_len > 0) {
+                    float* ser = cold_ptr(0);
+                    const int ms = cold_int(C_MAXSER);
+#pragma unroll
+                    for (int k = 0; k < D; ++k) ser[((b * ms) + st.series_len - 1) * N * D + n * D + k] = q[k];
+                }
+            }
+        }
+        if (rmask && BLS) {  // block-uniform
             const bool rs = tvalid && ((rmask >> t) & 1u);  // wave-uniform
             if (rs && valid) {
 #pragma unroll
@@ -1329,14 +1438,36 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
             IRM_STAMP(12);
             // --------------------------------------------------- accept
             if (accept == 1) {
+                if constexpr (BLS) {
 #pragma unroll
-                for (int k = 0; k < D; ++k) {
-                    q[k] = q2[k];
-                    v[k] = v2[k];
-                    aca[k] = cfac * aca[k] + step * dra[k];  // α recovery: Σ steps·[a'; b']
-                    acb[k] = cfac * acb[k] + step * drb[k];
+                    for (int k = 0; k < D; ++k) {
+                        q[k] = q2[k];
+                        v[k] = v2[k];
+                        aca[k] = cfac * aca[k] + step * dra[k];  // α recovery: Σ steps·[a'; b']
+                        acb[k] = cfac * acb[k] + step * drb[k];
+                    }
+                    cprod *= cfac;
+                } else {
+                    // α' = fl(fl(c·α) − fl(lr·G)) (optimizer_GD.py:81, 185) and its residual e' = −e·J/lr
+                    // for the next stage 1 (dP rows of this lane: stage 2 has been read)
+                    float er[D];
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        ab[k] = alpha_step(ab[k], cfac, lr, Gl[k], step, Gl[k], er[k]);
+                        q[k] = q2[k];
+                        v[k] = v2[k];
+                    }
+                    if (valid) {
+                        const float ne = -1.f / lr;
+#pragma unroll
+                        for (int k = 0; k < D; ++k) {
+                            float z = 0.f;
+#pragma unroll
+                            for (int l = 0; l < D; ++l) z = fmaf(er[l], cold[C_J + l * D + k], z);
+                            dP[n * kLd + t * D + k] = ne * z;
+                        }
+                    }
                 }
-                cprod *= cfac;
             }
             // extended-vis snapshot after every non-breaking inner iteration
             // (optimizer_GD.py:153-154, optimizer_BLS.py:106-107)
@@ -1467,31 +1598,6 @@ __device__ __forceinline__ void ered_store_wpl(const bool (&live)[WPL], const fl
             q[5] = oa;
         }
     }
-}
-
-// A value the compiler may not fuse into a neighbouring operation (hipcc contracts a·b − c into
-// an fma even under `#pragma clang fp contract(off)` when the product comes from __fmul_rn).
-__device__ __forceinline__ float unfused(float x) {
-    asm("" : "+v"(x));
-    return x;
-}
-
-// One fp32 α element of the reference's GD / BLS update and its rounding residual:
-//   α' = fl(fl(c·α) − fl(lr·ĝ))                        (optimizer_GD.py:81, optimizer_BLS.py:139)
-//   e  = α' − (c·α − step·G)  exactly (to fp32 rounding of e itself), where c·[T; V] − step·F·y'
-//        is the waypoint-space update the kernel applies (ĝ = G for GD, G/‖G‖ for BLS).
-// Products and the subtraction are rounded separately (the reference's arithmetic, no fma); the
-// residuals come from fma (c·α − fl(c·α) is exact) and TwoSum.
-__device__ __forceinline__ float alpha_step(float al, float c, float lr, float gh, float step, float G, float& e) {
-    const float p1 = unfused(c * al), p2 = unfused(lr * gh);
-    const float an = unfused(p1 - p2);
-    const float ep1 = fmaf(c, al, -p1);                 // c·α − p1
-    const float bb = an - p1;                           // TwoSum(p1, −p2) = an + es
-    const float es = (p1 - (an - bb)) + (-p2 - bb);
-    const float p = unfused(step * G);
-    const float ep = fmaf(step, G, -p);                 // step·G − p
-    e = (((p - p2) - es) + ep) - ep1;                   // α' − (c·α − step·G)
-    return an;
 }
 
 // Control flows of the lean kernel: the GD single loop (optimizer_GD.py:68-97, the bench path), the

@@ -166,13 +166,15 @@ ITER_COIN_FLIP = 5.0
 
 
 def check_iterations(tag, grad_evals):
-    """Gradient evaluations (= executed inner iterations) inside [0.7·min, 1.3·max] of the reference
-    with correctly rounded matmuls (its ±1-ulp runs).  With the reference's fp32 BLAS matmuls the
-    dual-loop counts are set by that summation noise (gd_n50: 272-334 with BLAS, 760 with exact
-    matmuls — the same algorithm), so the band is taken on the arithmetic this build uses."""
-    calls = e2e_reference(tag)["xm"]["grad_calls"].astype(float)
+    """Gradient evaluations (= executed inner iterations) inside [0.7·min, 1.3·max] of the reference's
+    runs — its ±1-ulp ensembles with its fp32 BLAS matmuls and with correctly rounded ones.  The
+    dual-loop counts are set by summation noise: gd_n50 takes 272-334 gradient calls with BLAS
+    matmuls and 760 with exact ones, gd_n500 188-191 and 399-402 — the same algorithm — so the band
+    spans both arithmetics (this build's G is a rank-32 fp32 MFMA contraction, between the two)."""
+    r = e2e_reference(tag)
+    calls = np.concatenate([r[v]["grad_calls"] for v in r]).astype(float)
     lo, hi = (1 - ITER_BAND) * calls.min(), (1 + ITER_BAND) * calls.max()
-    print(f"{tag}: grad evals {int(grad_evals)} (ref, exact matmuls: [{int(calls.min())}, {int(calls.max())}])")
+    print(f"{tag}: grad evals {int(grad_evals)} (ref, BLAS / exact matmuls: [{int(calls.min())}, {int(calls.max())}])")
     if calls.max() > ITER_COIN_FLIP * max(calls.min(), 1.0):
         return
     assert lo <= float(grad_evals) <= hi, (tag, grad_evals, calls)
