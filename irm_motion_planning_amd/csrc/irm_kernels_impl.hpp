@@ -480,25 +480,42 @@ __device__ void eval_exact(const KParams& P, const float* __restrict__ Xa, int n
     for (int d = 0; d < D; ++d) aq[d] = av[d] = 0.0;
     const float* kt = (Kt ? Kt : P.Kt) + n;
     const float* dkt = (dKt ? dKt : P.dKt) + n;
-    // K / dK rows come from L2 / HBM: 8 rows in flight per batch (the sum stays in the sequential
-    // order m = 0, 1, …, N−1 of the oracle)
+    // K / dK rows come from L2 / HBM: software-pipelined batches of 8 rows (the next batch's 16
+    // loads are in flight while this one is summed; the sum stays in the sequential order
+    // m = 0, 1, …, N−1 of the oracle)
     constexpr int U = 8;
-    int m0 = 0;
-    for (; m0 + U <= N; m0 += U) {
+    const int nb = N / U;
+    int m0 = nb * U;
+    if (nb > 0) {
         float kq[U], kv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            kq[u] = kt[(size_t)(m0 + u) * N];  // K[n][m]
-            kv[u] = dkt[(size_t)(m0 + u) * N]; // dK[n][m]
+            kq[u] = kt[(size_t)u * N];
+            kv[u] = dkt[(size_t)u * N];
         }
+        for (int bi = 0; bi < nb; ++bi) {
+            const int mb = bi * U;
+            float nq[U], nv[U];
+            const int mn = (bi + 1 < nb) ? mb + U : mb;  // (the last batch re-reads itself: no branch)
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const float* xr = Xa + (m0 + u) * rs;
+            for (int u = 0; u < U; ++u) {
+                nq[u] = kt[(size_t)(mn + u) * N];   // K[n][m]
+                nv[u] = dkt[(size_t)(mn + u) * N];  // dK[n][m]
+            }
 #pragma unroll
-            for (int d = 0; d < D; ++d) {
-                const double x = (double)xr[d * cs];
-                aq[d] = fma((double)kq[u], x, aq[d]);
-                av[d] = fma((double)kv[u], x, av[d]);
+            for (int u = 0; u < U; ++u) {
+                const float* xr = Xa + (mb + u) * rs;
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    const double x = (double)xr[d * cs];
+                    aq[d] = fma((double)kq[u], x, aq[d]);
+                    av[d] = fma((double)kv[u], x, av[d]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                kq[u] = nq[u];
+                kv[u] = nv[u];
             }
         }
     }
