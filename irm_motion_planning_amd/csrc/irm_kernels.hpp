@@ -162,7 +162,10 @@ enum ColdWord : int {
     C_J = 192,      // J, D×D
     kColdWords = 256
 };
-// lean: the layout of k_lean (stage-1 partials [split][column][r], stride RP + 8) instead of
+// column stride of k_lean's stage-1 partials ([split][column][r]): ≡ 8 mod 64 like its other strides
+// (conflict-free b128 tile reads and stores with the row swizzle r ^ (c & 4), see k_lean)
+__host__ __device__ constexpr int lean_ldy(int RP) { return RP + 8 + (64 - (RP + 8) % 64 + 8) % 64; }
+// lean: the layout of k_lean (stage-1 partials [split][column][r], stride lean_ldy(RP)) instead of
 // k_optimize's [split][r][column] (stride kLd) — 640 instead of 544 floats per split at RP = 32,
 // which decides whether N = 512 fits the general kernel's 160 KiB.
 __host__ __device__ constexpr Head plan_head(int MP, int RP, int nsplit, bool optimizer, bool lean = false) {
@@ -173,7 +176,7 @@ __host__ __device__ constexpr Head plan_head(int MP, int RP, int nsplit, bool op
     H.Ypart = H.Ymix = 0;
     if (optimizer) {
         H.Ypart = off;
-        off += al4(nsplit * (lean ? 16 * (RP + 8) : RP * kLd));
+        off += al4(nsplit * (lean ? 16 * lean_ldy(RP) : RP * kLd));
         H.Ymix = off;
         off += al4(RP * kLd);
     }
@@ -246,7 +249,7 @@ __host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, in
     e.eb = off;
     off += al4(16 * lean_ld(NK));
     e.zp = off;
-    off += al4(nsplit * 16 * (RP + 8));
+    off += al4(nsplit * 16 * lean_ldy(RP));
     e.gb = off;
     off += al4(16 * lean_ld(NK));
     e.total = off;

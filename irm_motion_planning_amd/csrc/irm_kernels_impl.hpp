@@ -1685,8 +1685,14 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     const float* VN = VL ? smem + LX.vn : P.VNp;
 
     const int KQ1 = MP / 16, KQa = NK / 16, MT1 = RP / 16, KQ2 = RP / 16, MT2 = MP / 16, MTG = NK / 16;
-    const int ldx = MP + 8, ldy = RP + 8, lde = lean_ld(NK);  // column strides
+    const int ldx = MP + 8, ldy = lean_ldy(RP), lde = lean_ld(NK);  // column strides, all ≡ 8 mod 64
     const int cl = lane & 15, r4 = 4 * (lane >> 4);  // MFMA column / first of 4 rows of this lane
+    // Bank swizzle of every [column][row] buffer: row r of column c lives at r ^ (c & 4) (the 4-row
+    // quads of a 16-row group swap pairwise in columns 4-7 / 12-15).  With column strides ≡ 8 mod 64
+    // the MFMA tiles' ds_read_b128 (16-lane groups, 64 banks) and ds_write_b128 (8-lane groups, 32
+    // banks) are then both conflict-free; per-row accesses stay so (a column's rows only permute).
+    const int r4x = r4 ^ (cl & 4);
+    auto swz = [](int r, int c) { return r ^ (c & 4); };
     const bool has1 = wave < MT1 * nsplit;
     const int tile1 = wave % MT1, sp1 = wave / MT1;
     const int kq0 = (KQa * sp1) / nsplit, kq1 = (KQa * (sp1 + 1)) / nsplit;
@@ -1875,8 +1881,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                         ma += a[d] * P.J[k * D + d];
                         mb += bb[d] * P.J[k * D + d];
                     }
-                    X[(t * D + k) * ldx + n] = ma;
-                    X[(t * D + k) * ldx + NK + n] = mb;
+                    X[(t * D + k) * ldx + swz(n, t * D + k)] = ma;
+                    X[(t * D + k) * ldx + NK + swz(n, t * D + k)] = mb;
                     bfar |= (bb[k] != 0.f) & !endrow;  // branch-free
                 }
             }
@@ -1885,7 +1891,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     };
     auto stage1 = [&](bool full) {  // Ypart[sp] = Fᵀ·[a'; b'] over this wave's unit
         if (!has1) return;
-        const float* xl = X + cl * ldx + r4;
+        const float* xl = X + cl * ldx + r4x;
         constexpr bool kFix = S::KQU > 0 && S::KQU <= S1Q;
         constexpr int KQU = kFix ? S::KQU : S1Q;
         auto in = [&](int i) { return kFix ? i < KQU : kq0 + i < kq1; };
@@ -1934,12 +1940,12 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 }
             }
         }
-        *reinterpret_cast<f32x4*>(Ypart + (sp1 * 16 + cl) * ldy + tile1 * 16 + r4) = acc0 + acc1;
+        *reinterpret_cast<f32x4*>(Ypart + (sp1 * 16 + cl) * ldy + tile1 * 16 + r4x) = acc0 + acc1;
     };
     // z = V_Rᵀ·e' (the last accepted step's rounding residual), MT1 × nsplit units over the waves
     // from the top down (C3: waves 4-7, idle in the Fᵀ stage), operator from LDS / L2
     auto stage1z = [&]() {
-        const float* el = Eb + cl * lde + r4;
+        const float* el = Eb + cl * lde + r4x;
         for (int u = nwaves - 1 - wave; u < MT1 * nsplit; u += nwaves) {
             const int tile = u % MT1, sp = u / MT1;
             const int k0 = (KQa * sp) / nsplit, k1 = (KQa * (sp + 1)) / nsplit;
@@ -1953,7 +1959,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], bb[2], acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], bb[3], acc1, 0, 0, 0);
             }
-            *reinterpret_cast<f32x4*>(Zp + (sp * 16 + cl) * ldy + tile * 16 + r4) = acc0 + acc1;
+            *reinterpret_cast<f32x4*>(Zp + (sp * 16 + cl) * ldy + tile * 16 + r4x) = acc0 + acc1;
         }
     };
     // stage 2: dP = F·(Σ_s Ypart[s] + Σ_s Zp[s]) (the pending residual folded in), Gb = V_R·Σ_s Ypart[s]
@@ -1968,8 +1974,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             if (i < KQ2) {
                 f32x4 bz = {0.f, 0.f, 0.f, 0.f};
                 for (int sp = 0; sp < nsplit; ++sp) {
-                    by[i] += *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + cl) * ldy + i * 16 + r4);
-                    bz += *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + i * 16 + r4);
+                    by[i] += *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + cl) * ldy + i * 16 + r4x);
+                    bz += *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + i * 16 + r4x);
                 }
                 bt[i] = by[i] + bz;
             }
@@ -1990,7 +1996,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
         for (int j = 0; j < S2T; ++j) {
             if (wave + j * nwaves < MT2)
-                *reinterpret_cast<f32x4*>(dP + cl * ldx + (wave + j * nwaves) * 16 + r4) = acc[j];
+                *reinterpret_cast<f32x4*>(dP + cl * ldx + (wave + j * nwaves) * 16 + r4x) = acc[j];
         }
         // G tiles (waypoint rows of V_R·y''), from the top wave down
         for (int u = nwaves - 1 - wave; u < MTG; u += nwaves) {
@@ -2004,7 +2010,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     for (int m = 0; m < 4; ++m) ag = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], by[i][m], ag, 0, 0, 0);
                 }
             }
-            *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4) = ag;
+            *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4x) = ag;
         }
     };
     // this lane's direction rows Δ = (F·y'')·J for waypoint j (endpoint velocity rows through
@@ -2013,8 +2019,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         float ut[D], uv[D];
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-            ut[k] = dP[(t * D + k) * ldx + nn[j]];
-            uv[k] = dP[(t * D + k) * ldx + NK + nn[j]];
+            ut[k] = dP[(t * D + k) * ldx + swz(nn[j], t * D + k)];
+            uv[k] = dP[(t * D + k) * ldx + NK + swz(nn[j], t * D + k)];
             if constexpr (kHL) {
                 const int r = vl[j] ? nn[j] : 0;
                 ut[k] = fmaf(hL[r], e0[k], fmaf(hL[MP + r], e1[k], ut[k]));
@@ -2041,7 +2047,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         const int r = vl[j] ? nn[j] : 0;
         const float v0 = kHL ? hVL[r] : hv0[j], v1 = kHL ? hVL[NK + r] : hv1[j];
 #pragma unroll
-        for (int k = 0; k < D; ++k) G[k] = fmaf(v0, e0[k], fmaf(v1, e1[k], Gb[(t * D + k) * lde + r]));
+        for (int k = 0; k < D; ++k) G[k] = fmaf(v0, e0[k], fmaf(v1, e1[k], Gb[(t * D + k) * lde + swz(r, t * D + k)]));
     };
     auto snapshot = [&](irm_stats& st) {  // extended-vis frame after a non-breaking inner iteration
         if (rec && st.series_len < P.max_series) {
@@ -2122,8 +2128,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
         for (int k = 0; k < D; ++k) {
             const float* xc = X + (t * D + k) * ldx;
-            e0[k] = xc[NK];
-            e1[k] = xc[NK + N - 1];
+            e0[k] = xc[NK + swz(0, t * D + k)];
+            e1[k] = xc[NK + swz(N - 1, t * D + k)];
         }
         IRM_STAMP(0);
         if (dirr) {  // block-uniform
@@ -2144,7 +2150,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
                         for (int a = 0; a < D; ++a) {
                             float y = fmaf(fb0, e0[a], fb1 * e1[a]);
-                            for (int sp = 0; sp < nsplit; ++sp) y += Ypart[(sp * 16 + t * D + a) * ldy + li];
+                            for (int sp = 0; sp < nsplit; ++sp) y += Ypart[(sp * 16 + t * D + a) * ldy + swz(li, t * D + a)];
                             g2 = fmaf(y, y, g2);
                             sa += y;
                         }
@@ -2189,7 +2195,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
                         for (int k = 0; k < D; ++k) {
                             X[(t * D + k) * ldx + nn[j]] = al[j][k];
-                            Eb[(t * D + k) * lde + nn[j]] = 0.f;  // absorbed by the exact trajectory
+                            Eb[(t * D + k) * lde + swz(nn[j], t * D + k)] = 0.f;  // absorbed by the exact trajectory
                         }
                     }
                     if constexpr (BLS) {
@@ -2377,7 +2383,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                             for (int j = 0; j < WPL; ++j)
                                 if (vl[j])
 #pragma unroll
-                                    for (int k = 0; k < D; ++k) Eb[(t * D + k) * lde + nn[j]] = -pend[j][k] / sref;
+                                    for (int k = 0; k < D; ++k) Eb[(t * D + k) * lde + swz(nn[j], t * D + k)] = -pend[j][k] / sref;
                         } else {
                             more = true;
                         }
@@ -2418,9 +2424,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                         v[j][k] = v2[j][k];
                         if constexpr (BLS) {
                             pend[j][k] = er + keep * pend[j][k];
-                            if (vl[j]) Eb[(t * D + k) * lde + nn[j]] = nsr * pend[j][k];
+                            if (vl[j]) Eb[(t * D + k) * lde + swz(nn[j], t * D + k)] = nsr * pend[j][k];
                         } else {
-                            if (vl[j]) Eb[(t * D + k) * lde + nn[j]] = er * ne;
+                            if (vl[j]) Eb[(t * D + k) * lde + swz(nn[j], t * D + k)] = er * ne;
                         }
                     }
                 }
