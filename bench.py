@@ -37,6 +37,9 @@ CONFIGS = {
     "c2": ("single trajectory, N=128, 10 obstacles, BLS (BASELINE configs[1])", 1, 128, 3, 10, "bls"),
     # north_star's stated target shape: a batch of 7-DoF, 128-waypoint trajectories
     "c7": ("north_star target: 7-DoF arm, batch of 1024 per GPU, N=128, 11 obstacles, GD", 1024, 128, 7, 11, "gd"),
+    # the reference's default optimiser (main.py:27) on C3's batch: batched backtracking line search
+    "c3bls": ("batch of 1024 random start/goal trajectories, N=128, D=3, 11 shared obstacles, BLS "
+              "(the reference's default optimizer, main.py:27)", 1024, 128, 3, 11, "bls"),
     # diagnostic shapes (not BASELINE configurations): C3's batch at other trajectory lengths
     "c3n64": ("diagnostic: C3 batch at N=64", 1024, 64, 3, 11, "gd"),
     "c3n256": ("diagnostic: C3 batch at N=256", 1024, 256, 3, 11, "gd"),
@@ -68,7 +71,7 @@ def make_problem(cfg, world, rank):
         if O > len(OBSTACLES):  # diagnostic: shifted copies of the reference set
             reps = -(-O // len(OBSTACLES))
             obstacles = np.concatenate([OBSTACLES + 0.1 * i for i in range(reps)])[:O].astype(np.float32)
-        rs = np.random.default_rng({"c5": 4, "c7": 7}.get(cfg, 1))
+        rs = np.random.default_rng({"c5": 4, "c7": 7}.get(cfg, 1))  # c3bls: C3's problems
     start = rs.uniform(-0.5, 0.5, (Btot, D)).astype(np.float32)
     goal = rs.uniform(0.2, 1.6, (Btot, D)).astype(np.float32)
     if cfg == "c2":
@@ -95,7 +98,7 @@ def make_args(cfg, faithful, max_inner):
     return irm_main.parse_args(argv)
 
 
-def flops_per_iteration(N, D, O, R):
+def flops_per_iteration(N, D, O, R, split=False):
     """Algorithmic fp32 flops of one GD iteration of one trajectory.
 
     exec: what the lean kernel (k_lean: waypoint-space rank-R iteration with the reference's fp32
@@ -105,10 +108,16 @@ def flops_per_iteration(N, D, O, R):
     residual (14·N·D), the waypoint update (4·N·D), obstacle pairs (14·N·O), FK / Jacobian /
     penalties (24·N·D, sincos counted as 4 flops each).
     ref: SURVEY.md §8d's count of the reference formulation, 12N²D + 10ND² + 22NO.
+    split: (direction round, trial round) — a BLS inner iteration is one direction round (the MFMA
+    stages, the mixes, the α update of the accepted step) and one evaluation per line-search trial
+    (waypoint update, obstacle pairs, FK / Jacobian / penalties); GD = one of each.
     """
-    exec_f = 10 * R * N * D + 8 * N * D * D + 14 * N * D + 4 * N * D + 14 * N * O + 24 * N * D
+    dir_f = 10 * R * N * D + 8 * N * D * D + 14 * N * D
+    trial_f = 4 * N * D + 14 * N * O + 24 * N * D
     ref_f = 12 * N * N * D + 10 * N * D * D + 22 * N * O
-    return exec_f, ref_f
+    if split:
+        return dir_f, trial_f, ref_f
+    return dir_f + trial_f, ref_f
 
 
 def effective_tb(a, info, B):
@@ -155,7 +164,8 @@ def cpu_baseline(cfg, args, start, goal, obstacles, budget_s=12.0):
     _, st = orc.optimize_batch(None, start[:n], goal[:n], obstacles, n_threads=cores)
     dt = time.perf_counter() - t0
     iters = sum(s["grad_evals"] for s in st)
-    return {"value": iters / dt, "unit": "GD iterations/s", "cores": cores, "kind": "port",
+    return {"value": iters / dt, "unit": ("GD" if args.optimizer_name == "gd" else "BLS") + " iterations/s",
+            "cores": cores, "kind": "port",
             "value_1thread": st1[0]["grad_evals"] / t1,  # 1-thread and all-cores rates
             "sample": f"{n} of the {len(start)} rank-0 problems, full optimize() each ({iters} iterations, "
                       f"{dt:.2f} s wall on {cores} threads); 1-thread rate {st1[0]['grad_evals'] / t1:.1f} it/s"}
@@ -195,7 +205,10 @@ def config_record(a, args, desc, B, N, D, O, opt, world, info):
     return {
         "workload": f"{a.config}: {desc}",
         "batch_per_gpu": B, "global_batch": B * world, "n_timesteps": N, "n_joints": D, "n_obstacles": O,
-        "optimizer": opt, "mode": "faithful" if a.faithful else f"bench ({a.max_inner} fixed GD iterations)",
+        "optimizer": opt,
+        "mode": "faithful" if a.faithful else (f"bench ({a.max_inner} fixed GD iterations)" if opt == "gd" else
+                                               f"bench ({a.max_inner} fixed BLS inner iterations, each with its "
+                                               "line search)"),
         "gd_lr_first": float(args.gd_lr[0]),
         "overrides_vs_reference_defaults": overrides,
         "operator_rank": None if info is None else info["operator_rank"],
@@ -362,11 +375,14 @@ def main():
 
     st = stats_t.cpu().numpy()
     iters_rank = float(st[:, 2].sum())  # grad_evals = executed inner iterations
+    trials_rank = float(st[:, 4].sum())  # BLS line-search trials (one evaluation round each)
     elapsed_max, iters_all = aggregate(elapsed, iters_rank, world, cdev)
     value = iters_all * a.steps / elapsed_max
 
-    exec_f, ref_f = flops_per_iteration(N, D, O, info["operator_rank"])
-    launch_flops = exec_f * iters_rank
+    dir_f, trial_f, ref_f = flops_per_iteration(N, D, O, info["operator_rank"], split=True)
+    exec_f = dir_f + trial_f
+    # GD: one trial per iteration; BLS: the trials the line searches ran
+    launch_flops = dir_f * iters_rank + trial_f * (trials_rank if opt == "bls" else iters_rank)
     achieved = launch_flops / (kernel_ms * 1e-3) / 1e12
     dense_tflops = ref_f * iters_rank / (kernel_ms * 1e-3) / 1e12
     bytes_launch = B * (2 * D + 2 * N * D) * 4 + B * 32  # start/goal in; alpha/traj/stats out
@@ -374,7 +390,7 @@ def main():
     traffic, traffic_src = pmc_traffic(a.config) if canonical else (None, None)
     counted, counted_src = pmc_flops(a.config) if canonical else (None, None)
     result = {
-        "metric": "GD iterations/sec (batch of trajectories)",
+        "metric": ("GD" if opt == "gd" else "BLS") + " iterations/sec (batch of trajectories)",
         "value": value,
         "unit": "iterations/s",
         "n_gpus": world,
@@ -402,6 +418,7 @@ def main():
             "kernel_ms": kernel_ms,
             "flops_per_iteration": exec_f,
             "flops_per_launch": launch_flops,
+            "bls_trials_per_launch": trials_rank if opt == "bls" else None,
             # what the hardware issued, from rocprofv3 PMC counters of the same command
             # (MFMA + f32 VALU lane operations, padding lanes/columns included; tools/pmc_flops.sh)
             "counted_flops_per_launch": counted,

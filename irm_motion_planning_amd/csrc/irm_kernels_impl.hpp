@@ -160,11 +160,7 @@ __device__ __forceinline__ void store_tile(float* out, int tile, f32x4 acc, unsi
 // sin/cos for robot.py's joint angles: Cody-Waite reduction by π/2 (3-part
 // split, fma) and the cephes single-precision minimax polynomials on
 // [−π/4, π/4]; ≈1 ulp, branch-free.  |x| > 1e4 rad falls back to sincosf.
-__device__ __forceinline__ void sincos_fast(float x, float& sn, float& cs) {
-    if (__builtin_expect(fabsf(x) > 1.0e4f, 0)) {
-        sincosf(x, &sn, &cs);
-        return;
-    }
+__device__ __forceinline__ void sincos_poly(float x, float& sn, float& cs) {
     const float kf = rintf(x * 0.636619772f);
     float r = fmaf(kf, -1.57079637050628662109375f, x);
     r = fmaf(kf, 4.371138828673793e-08f, r);
@@ -178,6 +174,13 @@ __device__ __forceinline__ void sincos_fast(float x, float& sn, float& cs) {
     const float c0 = (q & 1) ? sp : cp;
     sn = (q & 2) ? -s0 : s0;
     cs = ((q + 1) & 2) ? -c0 : c0;
+}
+__device__ __forceinline__ void sincos_fast(float x, float& sn, float& cs) {
+    if (__builtin_expect(fabsf(x) > 1.0e4f, 0)) {
+        sincosf(x, &sn, &cs);
+        return;
+    }
+    sincos_poly(x, sn, cs);
 }
 
 template <int D>
@@ -198,13 +201,30 @@ struct WP {
 template <int D, bool WHOLE = false>
 __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)[D], const float (&v)[D],
                                               const float* __restrict__ ob, WP<D>& w) {
-    float cum = 0.f, fx = 0.f, fy = 0.f, Sx = 0.f, Sy = 0.f;
-    float xs[D], ys[D], px[D], py[D];
+    float fx = 0.f, fy = 0.f, Sx = 0.f, Sy = 0.f;
+    float xs[D], ys[D], px[D], py[D], cum[D], snv[D], csv[D];
+    bool big = false;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-        cum += q[d];
-        float sn, cs;
-        sincos_fast(cum, sn, cs);
+        cum[d] = (d ? cum[d - 1] : 0.f) + q[d];
+        big |= fabsf(cum[d]) > 1.0e4f;
+    }
+    // One wave-uniform branch for all joints: the D polynomial chains share a basic block (the
+    // scheduler interleaves them); a wave with any |angle| > 1e4 takes the per-lane form, whose
+    // small-angle lanes compute the same polynomial, so every lane's value is that of sincos_fast.
+#ifdef IRM_X_NOSC
+    big = true;
+#endif
+    if (__builtin_expect(__ballot(big) != 0ull, 0)) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) sincos_fast(cum[d], snv[d], csv[d]);
+    } else {
+#pragma unroll
+        for (int d = 0; d < D; ++d) sincos_poly(cum[d], snv[d], csv[d]);
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const float sn = snv[d], cs = csv[d];
         fx += P.link[d] * cs;
         fy += P.link[d] * sn;
         px[d] = fx;
@@ -234,10 +254,34 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
             ax2 += dx * u2;
             ay2 += dy * u2;
         };
-        for (int c = 0; c < nq; ++c) {
-            const f32x4 p0 = o4[2 * c], p1 = o4[2 * c + 1];
-            pair2(p0.xy, p0.zw);
-            pair2(p1.xy, p1.zw);
+#ifdef IRM_X_NOOBS
+        if (false) {
+#else
+        if (nq == 3) {  // 9-12 obstacles (the reference's 11): one straight-line block, all 12 rcps
+                        // issued back to back, then the sums in pair2's order
+#endif
+            f32x2 dx[6], dy[6], u[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const f32x4 p = o4[i];
+                dx[i] = fx2 - p.xy;
+                dy[i] = fy2 - p.zw;
+                const f32x2 e = dy[i] * dy[i] + (dx[i] * dx[i] + one);
+                u[i] = f32x2{__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
+            }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                cv2 += u[i];
+                const f32x2 u2 = u[i] * u[i];
+                ax2 += dx[i] * u2;
+                ay2 += dy[i] * u2;
+            }
+        } else {
+            for (int c = 0; c < nq; ++c) {
+                const f32x4 p0 = o4[2 * c], p1 = o4[2 * c + 1];
+                pair2(p0.xy, p0.zw);
+                pair2(p1.xy, p1.zw);
+            }
         }
         cv = 1.6f * (cv2.x + cv2.y);
         ax = -3.2f * (ax2.x + ax2.y);
@@ -637,6 +681,10 @@ __device__ __forceinline__ float unfused(float x) {
     asm("" : "+v"(x));
     return x;
 }
+
+// Smallest step a rounding residual is folded with (e' = −e/step): |e'| ≤ 1e-3·2^80 ≈ 1e21 stays
+// finite where a tiny BLS step (lr/‖G‖ after many rejected trials, or --gd-lr 0) would give ±inf.
+constexpr float kMinRefStep = 8.271806e-25f;  // 2^-80
 
 // One fp32 α element of the reference's GD / BLS update and its rounding residual:
 //   α' = fl(fl(c·α) − fl(lr·ĝ))                        (optimizer_GD.py:81, optimizer_BLS.py:139)
@@ -1475,7 +1523,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                         v[k] = v2[k];
                     }
                     if (valid) {
-                        const float ne = -1.f / lr;
+                        const float ne = -1.f / fmaxf(lr, kMinRefStep);
 #pragma unroll
                         for (int k = 0; k < D; ++k) {
                             float z = 0.f;
@@ -1790,7 +1838,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     int outer = 0, inner = 0, trial = 0;
     int phase = tvalid ? LP_STEP : LP_DONE;
     bool needs_dir = false, xdense = false;
-    const float nilr = -1.f / lr;  // GD single loop: e' = −e/lr (the dual loop recomputes per outer)
+    const float nilr = -1.f / fmaxf(lr, kMinRefStep);  // GD single loop: e' = −e/lr (the dual loop recomputes per outer)
 
     // evaluation of (q2, v2) with this trajectory's waves: wave partials + endpoint rows
     auto evaluate = [&](const float (&q2)[WPL][D], const float (&v2)[WPL][D], bool ext, float ljl_e,
@@ -2107,11 +2155,18 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     float dTl[BLS ? WPL : 1][D], dVl[BLS ? WPL : 1][D], Gl[BLS ? WPL : 1][D];  // BLS: latched direction
     // BLS: the rounding residual not yet in [T; V] (α units) and the reference step it is folded into
     // y'' with (e' = −pend/sref): trial j applies the fraction s_j/sref of it, the rest carries over
+    // (sref ≥ kMinRefStep: after a long run of rejected trials lr/‖G‖ can fall below 1e-38, where
+    // −pend/sref would overflow to ±inf and 0·inf = NaN; a clamped sref folds the residual with a
+    // finite scale and the trials apply their fraction s_j/sref ≪ 1 of it, the rest stays pending)
     float pend[BLS ? WPL : 1][D], sref = 1.f;
 #pragma unroll
     for (int j = 0; j < (BLS ? WPL : 1); ++j)
 #pragma unroll
         for (int k = 0; k < D; ++k) dTl[j][k] = dVl[j][k] = Gl[j][k] = pend[j][k] = 0.f;
+    // The second half of the waves (4-7: the younger partner on each SIMD) loses VALU arbitration to
+    // the older one in every phase; static priority for that half (MI355X_MICROARCH.md, two waves per
+    // SIMD, item 4): C3 +1.7 %.  Priority only reorders issue: results are unchanged.
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
     for (int par = 0;; par ^= 1) {
         const unsigned fl = fw[par];
         if constexpr (GD1) {
@@ -2378,7 +2433,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                         } else if (rejected_all) {
                             needs_dir = true;  // the same α: X still holds its gradient inputs
                             bfar = xdense;
-                            sref = lr / gnorm;  // refold the pending residual for the next trial series
+                            sref = fmaxf(lr / gnorm, kMinRefStep);  // refold the pending residual for the next trial series
 #pragma unroll
                             for (int j = 0; j < WPL; ++j)
                                 if (vl[j])
@@ -2393,13 +2448,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             if (accept) {
                 // α' = fl(fl(c·α) − fl(lr·ĝ)) (optimizer_GD.py:81, optimizer_BLS.py:139) and its residual
                 // for the next direction (GD: −e/lr folded into stage 2's y''; BLS: e, through dC)
-                const float ne = GD1 ? nilr : -1.f / stepj;
+                const float ne = GD1 ? nilr : -1.f / fmaxf(stepj, kMinRefStep);
                 // BLS: [T; V] took the fraction s_j/sref of the pending residual; the rest (scaled by
                 // c_j like α) stays pending with this trial's residual, refolded for the next direction
                 float keep = 0.f, nsr = 0.f;
                 if constexpr (BLS) {
                     keep = cj - stepj / sref;
-                    sref = lr / gnorm;  // the next trial 0's step (lr already ·β+): keep ≈ 0 there
+                    sref = fmaxf(lr / gnorm, kMinRefStep);  // the next trial 0's step (lr already ·β+): keep ≈ 0 there
                     nsr = -1.f / sref;
                 }
 #pragma unroll
@@ -2411,6 +2466,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     } else {
                         grad_alpha(j, e0, e1, G);
                     }
+                    // the D element chains first (one basic block, interleaved), then the residual stores
+                    float eo[D];
 #pragma unroll
                     for (int k = 0; k < D; ++k) {
                         float er;
@@ -2424,10 +2481,14 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                         v[j][k] = v2[j][k];
                         if constexpr (BLS) {
                             pend[j][k] = er + keep * pend[j][k];
-                            if (vl[j]) Eb[(t * D + k) * lde + swz(nn[j], t * D + k)] = nsr * pend[j][k];
+                            eo[k] = nsr * pend[j][k];
                         } else {
-                            if (vl[j]) Eb[(t * D + k) * lde + swz(nn[j], t * D + k)] = er * ne;
+                            eo[k] = er * ne;
                         }
+                    }
+                    if (vl[j]) {
+#pragma unroll
+                        for (int k = 0; k < D; ++k) Eb[(t * D + k) * lde + swz(nn[j], t * D + k)] = eo[k];
                     }
                 }
             }

@@ -32,7 +32,10 @@ CASES = [  # (name, config, faithful, batch, general kernel, optimizer override)
 
 def run(out):
     res = {}
+    only = os.environ.get("IRM_CASES")
     for name, cfg, faithful, B, general, opt in CASES:
+        if only and name not in only.split(","):
+            continue
         args = bench.make_args(cfg, faithful, 200)
         if opt:
             args.optimizer_name = opt
