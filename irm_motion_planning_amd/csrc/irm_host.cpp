@@ -522,8 +522,18 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
         RP = round_up(R, 16);
         c->trunc = (R < N) ? (float)(std::max(0.0, G[(size_t)order[R] * N + order[R]]) / l0) : 0.f;
         Vd.assign((size_t)N * RP, 0.0);
+        // Rank slot of component r.  At RP = 32 the second k-quad interleaves components 16-23 and
+        // 24-31 so that the lean kernel's MFMAs 2 and 3 of that quad (k-permuted fragments: MFMA j
+        // covers rows j, 4+j, 8+j, 12+j of a quad) see only components 24-31, whose singular values
+        // are at fp32 noise (σ_24/σ_0 ≈ 3e-8 at N = 128) — k_lean skips those two MFMAs (rank 24 in
+        // stage 2).  Every other use is a sum over all slots, so the order does not matter there.
+        auto slot = [&](int r) {
+            if (RP != 32 || r < 16) return r;
+            const int j = r - 16, hi = j >= 8, q = j & 7;  // q-th of the 8 components of its half
+            return 16 + 4 * (q >> 1) + (q & 1) + (hi ? 2 : 0);
+        };
         for (int i = 0; i < N; ++i)
-            for (int r = 0; r < R; ++r) Vd[(size_t)i * RP + r] = Vfull[(size_t)i * N + order[r]];
+            for (int r = 0; r < R; ++r) Vd[(size_t)i * RP + slot(r)] = Vfull[(size_t)i * N + order[r]];
     }
     c->R = R;
     c->RP = RP;

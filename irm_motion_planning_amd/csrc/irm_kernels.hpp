@@ -228,6 +228,9 @@ __host__ __device__ inline Plan plan_lds(const KParams& p, bool ops_lds, bool op
 // endpoint operator columns hL (2·MP), G's endpoint columns hV (2·NK), the V_R fragments (when
 // staged: vlds), the rounding residual rows e' ([column][waypoint], stride NK + 8), its stage-1
 // partials zp ([split][column][r], stride RP + 8) and the gradient rows G ([column][waypoint]).
+// k-splits of k_lean's residual projection z = V_Rᵀ·e' (rank 16: one row tile, see k_lean): twice
+// the stage-1 splits where the LDS allows (vlds shapes: N ≤ 128, D ≤ 3), so the units stay one per wave
+__host__ __device__ constexpr int lean_zsplit(int nsplit, bool vlds) { return vlds ? 2 * nsplit : nsplit; }
 struct LeanX {
     int hl, hv, vt, vn, eb, zp, gb, total;
 };
@@ -249,7 +252,7 @@ __host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, in
     e.eb = off;
     off += al4(16 * lean_ld(NK));
     e.zp = off;
-    off += al4(nsplit * 16 * lean_ldy(RP));
+    off += al4(lean_zsplit(nsplit, vlds) * 16 * lean_ldy(RP));
     e.gb = off;
     off += al4(16 * lean_ld(NK));
     e.total = off;

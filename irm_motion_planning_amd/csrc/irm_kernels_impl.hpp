@@ -1688,6 +1688,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     constexpr int WPTL = NWL / 64;    // waves per trajectory
     constexpr bool VL = lean_vlds(S::NK, D);  // V_R fragments staged in LDS (else read from L2)
     static_assert(NWL % 64 == 0, "whole waves per trajectory");
+    static_assert(S::RP == 32, "k_lean runs at operator rank 32 (stage 2's kR24 slot skip)");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const S sh(P);
     const Head H = plan_head(sh.MP, sh.RP, sh.NSPLIT, true, true);
@@ -1722,7 +1723,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     float* wp = smem + H.wp;
     unsigned* fw = reinterpret_cast<unsigned*>(smem + H.flags);
     float* obsL = smem + H.obs;
-    const int nsplit = sh.NSPLIT;
+    const int nsplit = sh.NSPLIT, zsplit = lean_zsplit(sh.NSPLIT, VL);
     const LeanX LX = lean_extra(plan_lds(P, false, true, true).total, MP, NK, RP, nsplit, VL);
     float* hL = smem + LX.hl;  // endpoint columns of F·Fᵀ (2·MP), read per round when WPL > 1
     float* hVL = smem + LX.hv; // G's endpoint columns (2·NK), read per round when WPL > 1
@@ -1990,14 +1991,16 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         }
         *reinterpret_cast<f32x4*>(Ypart + (sp1 * 16 + cl) * ldy + tile1 * 16 + r4x) = acc0 + acc1;
     };
-    // z = V_Rᵀ·e' (the last accepted step's rounding residual), MT1 × nsplit units over the waves
-    // from the top down (C3: waves 4-7, idle in the Fᵀ stage), operator from LDS / L2
+    // z = V_Rᵀ·e' (the last accepted step's rounding residual) at rank 16: the residual's components
+    // along singular directions 16-31 of [K; dK] are below σ_16/σ_0 ≈ 4e-4 of |L·e| ≈ 1e-4, i.e. under
+    // 1e-7 per step, so only V_R's first row tile is applied (half the MFMAs of rank 32; Zp rows 16-31
+    // stay zero).  zsplit k-ranges over the waves from the top down (C3: waves 4-7, idle in the Fᵀ
+    // stage), operator from LDS / L2.
     auto stage1z = [&]() {
         const float* el = Eb + cl * lde + r4x;
-        for (int u = nwaves - 1 - wave; u < MT1 * nsplit; u += nwaves) {
-            const int tile = u % MT1, sp = u / MT1;
-            const int k0 = (KQa * sp) / nsplit, k1 = (KQa * (sp + 1)) / nsplit;
-            const f32x4* ap = reinterpret_cast<const f32x4*>(VT) + (size_t)tile * KQa * 64 + lane;
+        for (int sp = nwaves - 1 - wave; sp < zsplit; sp += nwaves) {
+            const int k0 = (KQa * sp) / zsplit, k1 = (KQa * (sp + 1)) / zsplit;
+            const f32x4* ap = reinterpret_cast<const f32x4*>(VT) + lane;
             f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
             for (int kq = k0; kq < k1; ++kq) {
                 const f32x4 a = ap[(size_t)kq * 64];
@@ -2007,10 +2010,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], bb[2], acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], bb[3], acc1, 0, 0, 0);
             }
-            *reinterpret_cast<f32x4*>(Zp + (sp * 16 + cl) * ldy + tile * 16 + r4x) = acc0 + acc1;
+            *reinterpret_cast<f32x4*>(Zp + (sp * 16 + cl) * ldy + r4x) = acc0 + acc1;
         }
     };
-    // stage 2: dP = F·(Σ_s Ypart[s] + Σ_s Zp[s]) (the pending residual folded in), Gb = V_R·Σ_s Ypart[s]
+    // stage 2: dP = F·(Σ_s Ypart[s] + Σ_s Zp[s]) (the pending residual folded in), Gb = V_R·Σ_s Ypart[s],
+    // both at rank 24 (kR24): the host puts the singular components 24-31 (σ/σ_0 ≈ 3e-8, fp32 noise of
+    // the rank-32 factorisation) into the rank slots that MFMAs 2-3 of the second k-quad read, and
+    // those MFMAs are skipped (irm_host.cpp, slot()); k_lean always runs at R = RP = 32.
     auto stage2 = [&]() {
         f32x4 acc[S2T];
 #pragma unroll
@@ -2021,9 +2027,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             by[i] = bt[i] = f32x4{0.f, 0.f, 0.f, 0.f};
             if (i < KQ2) {
                 f32x4 bz = {0.f, 0.f, 0.f, 0.f};
-                for (int sp = 0; sp < nsplit; ++sp) {
+                for (int sp = 0; sp < nsplit; ++sp)
                     by[i] += *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + cl) * ldy + i * 16 + r4x);
-                    bz += *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + i * 16 + r4x);
+                if (i == 0) {  // z has rank 16: rows 0-15 only
+                    for (int sp = 0; sp < zsplit; ++sp)
+                        bz += *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + r4x);
                 }
                 bt[i] = by[i] + bz;
             }
@@ -2035,8 +2043,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 for (int j = 0; j < S2T; ++j) {
                     if (wave + j * nwaves < MT2) {
 #pragma unroll
-                        for (int m = 0; m < 4; ++m)
+                        for (int m = 0; m < 4; ++m) {
+                            if (i == 1 && m >= 2) continue;  // rank slots of components 24-31 (kR24)
                             acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][m], bt[i][m], acc[j], 0, 0, 0);
+                        }
                     }
                 }
             }
@@ -2055,7 +2065,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 if (i < KQ2) {
                     const f32x4 a = ap[(size_t)i * 64];
 #pragma unroll
-                    for (int m = 0; m < 4; ++m) ag = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], by[i][m], ag, 0, 0, 0);
+                    for (int m = 0; m < (i == 1 ? 2 : 4); ++m)  // kR24
+                        ag = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], by[i][m], ag, 0, 0, 0);
                 }
             }
             *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4x) = ag;

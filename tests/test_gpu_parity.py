@@ -190,6 +190,32 @@ def test_bls_without_outer_iterations_returns_init(max_outer):
         assert int(st["constraints_ok"][b]) == int(st_o["constraints_ok"])
 
 
+def test_bls_tiny_steps_stay_finite():
+    """Accepted BLS steps whose lr collapses far below 1e-38·‖G‖ (β+ = 1e-12, no early exit): the
+    kernel folds α's rounding residual into the next direction relative to a reference step that is
+    clamped at 2^-80 (kMinRefStep), so −pend/sref stays finite (unclamped it overflowed to ±inf and
+    0·inf gave NaN: tools/nan_diag.py, c7 problem 7).  The trial log must show steps under the clamp;
+    α / trajectories stay finite and the final loss agrees with the oracle's (rtol 1e-3)."""
+    argv = ("--bls-beta_plus", "1e-12", "--loop-loss-reduction=-1", "--max-outer-iteration", "2",
+            "--max-inner-iteration", "12")
+    c = ctx(*argv)
+    rng = np.random.default_rng(11)
+    s = rng.uniform(-0.5, 0.5, (8, 3)).astype(np.float32)
+    g = rng.uniform(0.2, 1.6, (8, 3)).astype(np.float32)
+    s[0], g[0] = START, GOAL
+    c.bls_trace_enable(512)
+    alpha, traj, st = c.optimize(s, g, obstacles())
+    tr = c.bls_trace(int(st["bls_trials"][0]))
+    assert np.isfinite(alpha).all() and np.isfinite(traj).all() and np.isfinite(st["final_loss"]).all()
+    step = tr[:, 3].astype(np.float64) / tr[:, 8]  # lr / ‖G‖ of every trial of problem 0
+    assert (step < 2.0 ** -80).any(), step.min()
+    orc = oracle_for(*argv)
+    a0 = c.init_alpha(s, g)
+    for b in range(8):
+        _, st_o = orc.optimize(a0[b], obstacles(), s[b], g[b])
+        assert abs(float(st["final_loss"][b]) - st_o["final_loss"]) <= 1e-3 * abs(st_o["final_loss"]), b
+
+
 def test_obstacle_stride_is_validated():
     """obstacle_stride must be 0 (shared table) or >= 2·O floats (irm.h); per-problem B×O×2 arrays
     get the stride 2·O by default in Context.optimize, and a shape/stride mismatch raises."""
