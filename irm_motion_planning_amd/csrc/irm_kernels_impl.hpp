@@ -2013,10 +2013,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             *reinterpret_cast<f32x4*>(Zp + (sp * 16 + cl) * ldy + r4x) = acc0 + acc1;
         }
     };
-    // stage 2: dP = F·(Σ_s Ypart[s] + Σ_s Zp[s]) (the pending residual folded in), Gb = V_R·Σ_s Ypart[s],
-    // both at rank 24 (kR24): the host puts the singular components 24-31 (σ/σ_0 ≈ 3e-8, fp32 noise of
-    // the rank-32 factorisation) into the rank slots that MFMAs 2-3 of the second k-quad read, and
-    // those MFMAs are skipped (irm_host.cpp, slot()); k_lean always runs at R = RP = 32.
+    // stage 2: dP = F·(Σ_s Ypart[s] + Σ_s Zp[s]) (the pending residual folded in) at rank 16 (kR16F),
+    // Gb = V_R·Σ_s Ypart[s] at rank 24 (kR24): the host puts the singular components 24-31 (σ/σ_0 ≈
+    // 3e-8, fp32 noise of the rank-32 factorisation) into the rank slots that MFMAs 2-3 of the second
+    // k-quad read, and those MFMAs are skipped (irm_host.cpp, slot()); k_lean always runs at RP = 32.
+    // The α iterate uses G (rank 24, the reference's gradient to fp32 resolution); the waypoint state
+    // follows the rank-16 direction, off L·α·J by ≲ 1.5e-7 of a step per step (the one-residual lag
+    // below is 1e-4), and every inner-loop end replaces it by eval_exact(α).
     auto stage2 = [&]() {
         f32x4 acc[S2T];
 #pragma unroll
@@ -2036,19 +2039,14 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 bt[i] = by[i] + bz;
             }
         }
+        // the waypoint direction F·(y'' + z) at rank 16: F_r·y''_r ∝ σ_r², (σ_16/σ_0)² ≈ 1.5e-7 (N = 128),
+        // i.e. the fp32 rounding level of the direction itself (kR16F)
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            if (i < KQ2) {
+        for (int j = 0; j < S2T; ++j) {
+            if (wave + j * nwaves < MT2) {
 #pragma unroll
-                for (int j = 0; j < S2T; ++j) {
-                    if (wave + j * nwaves < MT2) {
-#pragma unroll
-                        for (int m = 0; m < 4; ++m) {
-                            if (i == 1 && m >= 2) continue;  // rank slots of components 24-31 (kR24)
-                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2 + i][m], bt[i][m], acc[j], 0, 0, 0);
-                        }
-                    }
-                }
+                for (int m = 0; m < 4; ++m)
+                    acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2][m], bt[0][m], acc[j], 0, 0, 0);
             }
         }
 #pragma unroll
