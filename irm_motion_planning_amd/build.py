@@ -22,7 +22,10 @@ HEADERS = [os.path.join(CSRC, h) for h in ("irm_kernels.hpp", "irm_kernels_impl.
     [os.path.join(HERE, "..", "include", "irm.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
-CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-unused-function"]
+# -amdgpu-atomic-optimizer-strategy=None: every LDS atomic in the kernels is issued by one lane (flag
+# words); the optimizer's scan over the active lanes is a ~25-instruction waterfall per round there
+CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-unused-function",
+          "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
 FIX_SHAPES = [(3, 50), (3, 64), (3, 128), (3, 256), (7, 128), (7, 256)]  # IRM_FIX_SHAPES in irm_kernels_impl.hpp
 MAX_D = 8
 
@@ -84,7 +87,16 @@ def build(force=False, verbose=False, variant="", jobs=None):
         subprocess.check_call(cmd, cwd=CSRC)
 
     if "-DIRM_DEFAULT_SCHED" in extra:
-        todo = [[x for x in cmd if x not in ILP_SCHED] for cmd in todo]
+        def drop_sched(cmd):
+            out, i = [], 0
+            while i < len(cmd):
+                if cmd[i:i + 2] == ILP_SCHED:
+                    i += 2
+                    continue
+                out.append(cmd[i])
+                i += 1
+            return out
+        todo = [drop_sched(cmd) for cmd in todo]
     if todo:
         with ThreadPoolExecutor(jobs) as ex:
             list(ex.map(run, todo))
