@@ -200,7 +200,9 @@ struct WP {
 // returned as w.jx (with w.gx = 1, w.jy = w.gy = 0) so grad_waypoint is shared.
 template <int D, bool WHOLE = false>
 __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)[D], const float (&v)[D],
-                                              const float* __restrict__ ob, WP<D>& w) {
+                                              const float* __restrict__ ob, WP<D>& w,
+                                              const f32x4* oreg = nullptr) {  // oreg: the 12-obstacle
+                                                                              // table held in VGPRs
     float fx = 0.f, fy = 0.f, Sx = 0.f, Sy = 0.f;
     float xs[D], ys[D], px[D], py[D], cum[D], snv[D], csv[D];
     bool big = false;
@@ -263,7 +265,7 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
             f32x2 dx[6], dy[6], u[6];
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
-                const f32x4 p = o4[i];
+                const f32x4 p = oreg ? oreg[i] : o4[i];
                 dx[i] = fx2 - p.xy;
                 dy[i] = fy2 - p.zw;
                 const f32x2 e = dy[i] * dy[i] + (dx[i] * dx[i] + one);
@@ -1844,6 +1846,12 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     __syncthreads();
     for (int e = tid; e < MP * kLd; e += P.BT) X[e] = 0.f;
     const float* obs = obsL + (P.obs_stride ? t * obs_pitch(P.O) : 0);
+    // 9-12 obstacles (the reference's 11): the padded table in VGPRs for the whole launch (24 floats),
+    // so the per-round evaluation does not wait on its LDS reads
+    f32x4 oreg[6];
+    const bool obs_reg = ((P.O + 3) >> 2) == 3;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) oreg[i] = obs_reg ? reinterpret_cast<const f32x4*>(obs)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
     // replicated per-trajectory state
     float lsg = P.lsg0, ljl = P.ljl0;
     float lr = BLS ? P.bls_lr0 : P.gd_lr[0];
@@ -1860,7 +1868,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         float cvs[WPL], us = 0.f, tx = -INFINITY, tn = INFINITY, va = 0.f;
 #pragma unroll
         for (int j = 0; j < WPL; ++j) {
-            if (vl[j]) eval_waypoint<D>(P, q2[j], v2[j], obs, w[j]);
+            if (vl[j]) eval_waypoint<D>(P, q2[j], v2[j], obs, w[j], oreg);  // oreg: read only when nq == 3
             cvs[j] = w[j].cv;
             const float u = P.one_m_lmax * (w[j].cv * P.invN) + ljl_e * ((w[j].jp + w[j].jv) * P.invN);
             if (j == 0) {
