@@ -98,21 +98,23 @@ def make_args(cfg, faithful, max_inner):
     return irm_main.parse_args(argv)
 
 
-def flops_per_iteration(N, D, O, R, split=False):
+def flops_per_iteration(N, D, O, R, split=False, lean=True):
     """Algorithmic fp32 flops of one GD iteration of one trajectory.
 
-    exec: what the lean kernel (k_lean: waypoint-space rank-R iteration with the reference's fp32
-    α rounding) must do — stage 1 (y'' = Fᵀ[a; b]·Jᵀ, 2·R·N·D; the rounding residual z = V_Rᵀ·e',
-    2·R·N·D), stage 2 (F·(y'' + z), 2·2N·R·D; G = V_R·y'', 2·N·R·D), the Jᵀ / J mixes of the
-    gradient inputs and of the direction (2 × 2·2·N·D²), the α update with its error-free
-    residual (14·N·D), the waypoint update (4·N·D), obstacle pairs (14·N·O), FK / Jacobian /
-    penalties (24·N·D, sincos counted as 4 flops each).
+    exec: what the optimiser kernel (waypoint-space rank-R iteration with the reference's fp32 α
+    rounding) must do — stage 1 (y'' = Fᵀ[a; b]·Jᵀ, 2·R·N·D), the rounding residual z = V_Rᵀ·e'
+    (2·Rz·N·D), stage 2 (the direction F·(y'' + z), 2·2N·Rf·D; G = V_R·y'', 2·N·Rg·D) — k_lean at
+    R = 32 runs z and the direction at rank 16 and G at rank 24, k_optimize all at
+    R —, the Jᵀ / J mixes of the gradient inputs and of the direction (2 × 2·2·N·D²), the α update
+    with its error-free residual (14·N·D), the waypoint update (4·N·D), obstacle pairs (14·N·O),
+    FK / Jacobian / penalties (24·N·D, sincos counted as 4 flops each).
     ref: SURVEY.md §8d's count of the reference formulation, 12N²D + 10ND² + 22NO.
     split: (direction round, trial round) — a BLS inner iteration is one direction round (the MFMA
     stages, the mixes, the α update of the accepted step) and one evaluation per line-search trial
     (waypoint update, obstacle pairs, FK / Jacobian / penalties); GD = one of each.
     """
-    dir_f = 10 * R * N * D + 8 * N * D * D + 14 * N * D
+    Rz, Rf, Rg = (16, 16, 24) if (lean and R == 32) else (R, R, R)
+    dir_f = 2 * R * N * D + 2 * Rz * N * D + 4 * Rf * N * D + 2 * Rg * N * D + 8 * N * D * D + 14 * N * D
     trial_f = 4 * N * D + 14 * N * O + 24 * N * D
     ref_f = 12 * N * N * D + 10 * N * D * D + 22 * N * O
     if split:
@@ -379,7 +381,8 @@ def main():
     elapsed_max, iters_all = aggregate(elapsed, iters_rank, world, cdev)
     value = iters_all * a.steps / elapsed_max
 
-    dir_f, trial_f, ref_f = flops_per_iteration(N, D, O, info["operator_rank"], split=True)
+    kernel = optimiser_kernel(a, info, N, D, opt, B)
+    dir_f, trial_f, ref_f = flops_per_iteration(N, D, O, info["operator_rank"], split=True, lean="k_lean" in kernel)
     exec_f = dir_f + trial_f
     # GD: one trial per iteration; BLS: the trials the line searches ran
     launch_flops = dir_f * iters_rank + trial_f * (trials_rank if opt == "bls" else iters_rank)
@@ -414,7 +417,7 @@ def main():
             "frac": achieved / PEAK_FP32_TFLOPS,
             "traffic": traffic,
             "traffic_source": traffic_src,
-            "kernel": optimiser_kernel(a, info, N, D, opt, B),
+            "kernel": kernel,
             "kernel_ms": kernel_ms,
             "flops_per_iteration": exec_f,
             "flops_per_launch": launch_flops,

@@ -109,7 +109,10 @@ def test_bench_flop_model():
     exec_f, ref_f = bench.flops_per_iteration(128, 3, 11, 32)
     assert ref_f == 12 * 128 * 128 * 3 + 10 * 128 * 9 + 22 * 128 * 11 == 632320
     assert 0 < exec_f < ref_f
-    assert exec_f == 10 * 32 * 128 * 3 + 8 * 128 * 9 + 42 * 128 * 3 + 14 * 128 * 11 == 167936
+    # k_lean at R = 32: stage 1 rank 32, residual z and direction rank 16, G rank 24
+    assert exec_f == (2 * 32 + 2 * 16 + 4 * 16 + 2 * 24) * 128 * 3 + 8 * 128 * 9 + 42 * 128 * 3 + 14 * 128 * 11 == 124928
+    gen_f, _ = bench.flops_per_iteration(128, 3, 11, 32, lean=False)  # k_optimize: every stage at R
+    assert gen_f == 10 * 32 * 128 * 3 + 8 * 128 * 9 + 42 * 128 * 3 + 14 * 128 * 11 == 167936
 
 
 def test_bench_kernel_label_mirrors_dispatch():
