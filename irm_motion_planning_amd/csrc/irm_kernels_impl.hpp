@@ -41,13 +41,23 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // DPP row reductions (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
 // row_mirror) leave each 16-lane row reduced in all its lanes; the four
 // rows are then combined from v_readlane (uniform result, no LDS).
+// Every control used here is an in-row permutation (no lane reads outside its row), so the old value
+// is never kept: mov_dpp (old undefined, bound_ctrl) lets the compiler fold the move into the consuming
+// VALU op as a DPP source (v_add_f32_dpp …) instead of v_mov_b32 + v_mov_b32_dpp + the op.
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xF, 0xF, false));
+    static_assert(CTRL == 0xB1 || CTRL == 0x4E || CTRL == 0x141 || CTRL == 0x140, "in-row permutations only");
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 template <int CTRL>
 __device__ __forceinline__ int dppi(int v) {
-    return __builtin_amdgcn_update_dpp(v, v, CTRL, 0xF, 0xF, false);
+    static_assert(CTRL == 0xB1 || CTRL == 0x4E || CTRL == 0x141 || CTRL == 0x140, "in-row permutations only");
+    return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
+}
+// max of floats that are ≥ +0 or −inf, on their bit patterns (signed-int order = float order there):
+// no NaN canonicalisation, and the DPP move folds into v_max_i32_dpp
+__device__ __forceinline__ float maxpos(float a, float b) {
+    return __int_as_float(max(__float_as_int(a), __float_as_int(b)));
 }
 __device__ __forceinline__ float lanef(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
@@ -636,14 +646,14 @@ __device__ void grad_exact(const KParams& P, const float* __restrict__ Xa, int n
 // Lane 0 stores the wave's record at red[wave·8].
 __device__ __forceinline__ void ered_store(bool live, float cv, float us, float tx, float tn, float va, bool ext,
                                            int n0, float* red, int wave) {
-    float m = live ? cv : -INFINITY, s = live ? us : 0.f;
-    m = fmaxf(m, dppf<0xB1>(m));
+    float m = live ? cv : -INFINITY, s = live ? us : 0.f;  // cv ≥ +0 (a sum of reciprocals): maxpos
+    m = maxpos(m, dppf<0xB1>(m));
     s += dppf<0xB1>(s);
-    m = fmaxf(m, dppf<0x4E>(m));
+    m = maxpos(m, dppf<0x4E>(m));
     s += dppf<0x4E>(s);
-    m = fmaxf(m, dppf<0x141>(m));
+    m = maxpos(m, dppf<0x141>(m));
     s += dppf<0x141>(s);
-    m = fmaxf(m, dppf<0x140>(m));
+    m = maxpos(m, dppf<0x140>(m));
     s += dppf<0x140>(s);
     // cross-row combine with the CDNA4 row / half swaps: (r0 ∘ r1) ∘ (r2 ∘ r3) in every lane, the
     // association of the readlane form (lanes 0, 16, 32, 48)
@@ -651,11 +661,11 @@ __device__ __forceinline__ void ered_store(bool live, float cv, float us, float 
     {
         auto pm = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
         auto ps = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
-        const float m2 = fmaxf(__uint_as_float(pm[0]), __uint_as_float(pm[1]));
+        const float m2 = maxpos(__uint_as_float(pm[0]), __uint_as_float(pm[1]));
         const float s2 = __uint_as_float(ps[0]) + __uint_as_float(ps[1]);
         auto qm = __builtin_amdgcn_permlane32_swap(__float_as_uint(m2), __float_as_uint(m2), false, false);
         auto qs = __builtin_amdgcn_permlane32_swap(__float_as_uint(s2), __float_as_uint(s2), false, false);
-        wm = fmaxf(__uint_as_float(qm[0]), __uint_as_float(qm[1]));
+        wm = maxpos(__uint_as_float(qm[0]), __uint_as_float(qm[1]));
         ws = __uint_as_float(qs[0]) + __uint_as_float(qs[1]);
     }
     const unsigned long long hit = __ballot(live && cv == wm);
