@@ -389,6 +389,29 @@ __device__ __forceinline__ void grad_waypoint(const KParams& P, const WP<D>& w, 
     }
 }
 
+// grad_waypoint with the start/goal rows' selection precomputed per lane (loop-invariant): epf = 1 on
+// rows 0 and N−1 (else 0), tg = the row's target (start on row 0, goal on row N−1).  The same values
+// as grad_waypoint wherever a term is non-zero (an interior row's 0·(q − tg) may be −0).
+template <int D>
+__device__ __forceinline__ void grad_waypoint_ep(const KParams& P, const WP<D>& w, const float (&q)[D],
+                                                 const float (&v)[D], int n, int idx, float lsg, float ljl,
+                                                 float epf, const float (&tg)[D], float (&a)[D], float (&b)[D]) {
+    const float wt = (n == idx ? P.lam_max : 0.f) + P.one_m_lmax * P.invN;
+    const float wx = wt * w.gx, wy = wt * w.gy;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const float sgp = epf * (q[d] - tg[d]);
+        const float sgv = epf * v[d];
+        float jpg = 0.f, jvg = 0.f;
+        const bool m = (q[d] > P.thr_hi) || (q[d] < P.thr_lo);
+        if (!P.cvdl || m) jpg = ((q[d] - P.mean_pos) * P.inv_std2) * P.invN;
+        const bool mv = fabsf(v[d]) > P.thr_v;
+        if (!P.cvdl || mv) jvg = (v[d] * P.inv_vmax2) * P.invN;
+        a[d] = (wx * w.jx[d] + wy * w.jy[d]) + lsg * sgp + ljl * jpg;
+        b[d] = lsg * sgv + ljl * jvg;
+    }
+}
+
 // Result of one cost evaluation of one trajectory (reduced over waypoints).
 struct EvalOut {
     float loss, ds, dg, vs, vg, tmax, tmin, vabs;
@@ -1838,6 +1861,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         s[k] = tvalid ? P.start[b * D + k] : 0.f;
         g[k] = tvalid ? P.goal[b * D + k] : 0.f;
     }
+    float epf[WPL], tg[WPL][D];  // start/goal rows of grad_waypoint_ep, per lane
+#pragma unroll
+    for (int j = 0; j < WPL; ++j) {
+        epf[j] = (nn[j] == 0 || nn[j] == N - 1) ? 1.f : 0.f;
+#pragma unroll
+        for (int k = 0; k < D; ++k) tg[j][k] = (nn[j] == N - 1) ? g[k] : s[k];
+    }
 #pragma unroll
     for (int j = 0; j < WPL; ++j) {
 #pragma unroll
@@ -1951,8 +1981,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             const int n = nn[j];
             if (vl[j]) {
                 float a[D], bb[D];
-                grad_waypoint<D>(P, w[j], q2[j], v2[j], n, cidx, lsg_e, ljl_e, s, g, a, bb);
-                const bool endrow = (n == 0 || n == N - 1);
+                grad_waypoint_ep<D>(P, w[j], q2[j], v2[j], n, cidx, lsg_e, ljl_e, epf[j], tg[j], a, bb);
+                const bool endrow = epf[j] != 0.f;
 #pragma unroll
                 for (int k = 0; k < D; ++k) {
                     float ma = 0.f, mb = 0.f;
