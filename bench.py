@@ -278,7 +278,8 @@ def dry_run(a, world, rank):
     if world > 1:
         dist.all_gather(shards, shard)
     if rank == 0:
-        print(json.dumps({"metric": "GD iterations/sec (batch of trajectories)", "value": None, "dry_run": True,
+        print(json.dumps({"metric": ("GD" if opt == "gd" else "BLS") + " iterations/sec (batch of trajectories)",
+                          "value": None, "dry_run": True,
                           "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                           "config": config_record(a, args, desc, B, N, D, O, opt, world, None),
                           "obstacles_equal_rank0": bool(same.item() == 1.0),

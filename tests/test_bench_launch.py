@@ -38,3 +38,26 @@ def test_single_rank_default():
     ov = r["config"]["overrides_vs_reference_defaults"]
     assert ov["gd_lr"] == [1e-3] and ov["max_outer_iteration"] == 1
     assert r["config"]["gd_lr_first"] == 1e-3
+
+
+def test_batched_bls_config():
+    """c3bls: C3's 1024 problems with the reference's default optimiser (BLS); the line reports BLS
+    inner iterations and records the bench-mode overrides like the GD configs."""
+    r = _bench("--dry-run", "--config", "c3bls")
+    assert r["metric"] == "BLS iterations/sec (batch of trajectories)"
+    assert r["config"]["optimizer"] == "bls" and r["config"]["global_batch"] == 1024
+    assert r["config"]["mode"].startswith("bench (200 fixed BLS inner iterations")
+    assert r["iterations_all"] == 1024 * 200
+    r = _bench("--dry-run", "--config", "c3bls", "--faithful")
+    assert r["config"]["mode"] == "faithful" and r["config"]["overrides_vs_reference_defaults"] == {}
+
+
+def test_bls_flop_model_counts_trials():
+    """BLS lines: one direction round per inner iteration plus one evaluation per line-search trial."""
+    import importlib
+    sys.path.insert(0, REPO)
+    bench = importlib.import_module("bench")
+    d, t, ref = bench.flops_per_iteration(128, 3, 11, 32, split=True)
+    e, ref2 = bench.flops_per_iteration(128, 3, 11, 32)
+    assert e == d + t and ref == ref2
+    assert t == 4 * 128 * 3 + 14 * 128 * 11 + 24 * 128 * 3  # update + obstacle pairs + FK / penalties
