@@ -34,8 +34,6 @@ VARIANTS = {
     "prof": ("libirm_hip_prof.so", ["-DIRM_PHASE_PROFILE"]),
     # every unit with the default scheduler (tools/sched_check.py compares it bit for bit)
     "defsched": ("libirm_hip_defsched.so", ["-DIRM_DEFAULT_SCHED"]),
-    # experiment builds (bench A/B on the GPU box with IRM_LIB=…)
-    "exp1": ("libirm_hip_exp1.so", ["-DIRM_EXP1"]),
 }
 
 
@@ -116,7 +114,7 @@ def asm(out_dir, inst=("-DIRM_INST_FIX_D=3", "-DIRM_INST_FIX_N=128")):
 if __name__ == "__main__":
     jobs = int(sys.argv[sys.argv.index("-j") + 1]) if "-j" in sys.argv else None
     build(force="--force" in sys.argv, verbose=True, jobs=jobs)
-    for v in VARIANTS:
+    for v in VARIANTS:  # e.g. --defsched (tools/sched_check.py)
         if v and v != "prof" and f"--{v}" in sys.argv:
             build(force="--force" in sys.argv, variant=v, verbose=True, jobs=jobs)
     if "--prof" in sys.argv:
