@@ -1671,22 +1671,22 @@ __device__ __forceinline__ void ered_store_wpl(const bool (&live)[WPL], const fl
             }
         }
         const bool any = live[0];
-        float m = best, s = any ? us : 0.f;
-        m = fmaxf(m, dppf<0xB1>(m));
+        float m = best, s = any ? us : 0.f;  // best ≥ +0 or −inf: maxpos (see ered_store)
+        m = maxpos(m, dppf<0xB1>(m));
         s += dppf<0xB1>(s);
-        m = fmaxf(m, dppf<0x4E>(m));
+        m = maxpos(m, dppf<0x4E>(m));
         s += dppf<0x4E>(s);
-        m = fmaxf(m, dppf<0x141>(m));
+        m = maxpos(m, dppf<0x141>(m));
         s += dppf<0x141>(s);
-        m = fmaxf(m, dppf<0x140>(m));
+        m = maxpos(m, dppf<0x140>(m));
         s += dppf<0x140>(s);
         auto pm = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
         auto ps = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
-        const float m2 = fmaxf(__uint_as_float(pm[0]), __uint_as_float(pm[1]));
+        const float m2 = maxpos(__uint_as_float(pm[0]), __uint_as_float(pm[1]));
         const float s2 = __uint_as_float(ps[0]) + __uint_as_float(ps[1]);
         auto qm = __builtin_amdgcn_permlane32_swap(__float_as_uint(m2), __float_as_uint(m2), false, false);
         auto qs = __builtin_amdgcn_permlane32_swap(__float_as_uint(s2), __float_as_uint(s2), false, false);
-        const float wm = fmaxf(__uint_as_float(qm[0]), __uint_as_float(qm[1]));
+        const float wm = maxpos(__uint_as_float(qm[0]), __uint_as_float(qm[1]));
         const float ws = __uint_as_float(qs[0]) + __uint_as_float(qs[1]);
         int idx = 0x7fffffff;
 #pragma unroll
