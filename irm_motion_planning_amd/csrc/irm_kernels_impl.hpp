@@ -199,6 +199,7 @@ struct WP {
     float jp, jv;            // masked joint-position / joint-velocity penalty terms
     float tx, tn, va;        // max/min joint position, max |joint velocity|
     float jx[D], jy[D];      // end-effector Jacobian row
+    float fx, fy;            // end-effector position (eval_waypoint<…, POT = false>: potential not yet added)
 };
 
 // robot.py:29-36 (fk), 75-87 (jacobian); environment.py:46-58
@@ -208,7 +209,9 @@ struct WP {
 // effector only.  Its gradient w.r.t. angle k is Σ_{l≥k} (X_l·GX_l + Y_l·GY_l)
 // with (X_l, Y_l) = L_l·(−sin c_l, cos c_l) and GX_l = Σ_{j≥l} ∂cost/∂p_j; it is
 // returned as w.jx (with w.gx = 1, w.jy = w.gy = 0) so grad_waypoint is shared.
-template <int D, bool WHOLE = false>
+// POT = false (end-effector cost only): everything but the obstacle potential, whose inputs are left
+// in w.fx / w.fy (potential_pair evaluates two waypoints' potentials in one pass over the obstacles).
+template <int D, bool WHOLE = false, bool POT = true>
 __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)[D], const float (&v)[D],
                                               const float* __restrict__ ob, WP<D>& w,
                                               const f32x4* oreg = nullptr) {  // oreg: the 12-obstacle
@@ -308,7 +311,12 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
             w.jx[d] = (xs[d] + Sx) - Cx;
             w.jy[d] = (ys[d] + Sy) - Cy;
         }
-        potential(fx, fy, w.cv, w.gx, w.gy);
+        if constexpr (POT) {
+            potential(fx, fy, w.cv, w.gx, w.gy);
+        } else {
+            w.fx = fx;
+            w.fy = fy;
+        }
     } else {
         float cvt = 0.f, gxj[D], gyj[D];
 #pragma unroll
@@ -348,6 +356,40 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
     w.tx = tx;
     w.tn = tn;
     w.va = va;
+}
+
+// The obstacle potential of two waypoints (w0.fx/fy, w1.fx/fy) in one pass over the LDS obstacle table:
+// each obstacle pair is loaded once and both waypoints' terms are formed from it (independent chains
+// that interleave).  Per waypoint the arithmetic and the accumulation order are eval_waypoint's.
+template <int D>
+__device__ __forceinline__ void potential_pair(const KParams& P, const float* __restrict__ ob, WP<D>& w0, WP<D>& w1) {
+    const f32x4* o4 = reinterpret_cast<const f32x4*>(ob);
+    const int nq = (P.O + 3) >> 2;
+    f32x2 cv0 = {0.f, 0.f}, ax0 = {0.f, 0.f}, ay0 = {0.f, 0.f}, cv1 = cv0, ax1 = cv0, ay1 = cv0;
+    const f32x2 x0 = {w0.fx, w0.fx}, y0 = {w0.fy, w0.fy}, x1 = {w1.fx, w1.fx}, y1 = {w1.fy, w1.fy};
+    const f32x2 one = {1.f, 1.f};
+    auto pair2 = [&](const f32x2& fx2, const f32x2& fy2, f32x2 ox, f32x2 oy, f32x2& cv2, f32x2& ax2, f32x2& ay2) {
+        const f32x2 dx = fx2 - ox, dy = fy2 - oy;
+        const f32x2 e = dy * dy + (dx * dx + one);
+        const f32x2 u = {__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
+        cv2 += u;
+        const f32x2 u2 = u * u;
+        ax2 += dx * u2;
+        ay2 += dy * u2;
+    };
+    for (int c = 0; c < nq; ++c) {
+        const f32x4 p0 = o4[2 * c], p1 = o4[2 * c + 1];
+        pair2(x0, y0, p0.xy, p0.zw, cv0, ax0, ay0);
+        pair2(x1, y1, p0.xy, p0.zw, cv1, ax1, ay1);
+        pair2(x0, y0, p1.xy, p1.zw, cv0, ax0, ay0);
+        pair2(x1, y1, p1.xy, p1.zw, cv1, ax1, ay1);
+    }
+    w0.cv = 1.6f * (cv0.x + cv0.y);
+    w0.gx = -3.2f * (ax0.x + ax0.y);
+    w0.gy = -3.2f * (ay0.x + ay0.y);
+    w1.cv = 1.6f * (cv1.x + cv1.y);
+    w1.gx = -3.2f * (ax1.x + ax1.y);
+    w1.gy = -3.2f * (ay1.x + ay1.y);
 }
 
 // eval_waypoint with the cost variant chosen at run time (host-API kernels, DynShape optimiser).
@@ -1735,6 +1777,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     constexpr int WPTL = NWL / 64;    // waves per trajectory
     constexpr bool VL = lean_vlds(S::NK, D);  // V_R fragments staged in LDS (else read from L2)
     static_assert(NWL % 64 == 0, "whole waves per trajectory");
+    static_assert(WPL == 1 || (WPL == 2 && S::kNW > 0 && S::kNW == S::NK),
+                  "two waypoints per lane: every lane's waypoints exist (N a multiple of 64)");
     static_assert(S::RP == 32, "k_lean runs at operator rank 32 (stage 2's kR24 slot skip)");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const S sh(P);
@@ -1906,9 +1950,16 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     auto evaluate = [&](const float (&q2)[WPL][D], const float (&v2)[WPL][D], bool ext, float ljl_e,
                         WP<D> (&w)[WPL]) {
         float cvs[WPL], us = 0.f, tx = -INFINITY, tn = INFINITY, va = 0.f;
+        if constexpr (WPL == 2) {  // both waypoints' obstacle terms in one pass (vl[0] = vl[1] = tvalid here)
+            if (tvalid) {
+                eval_waypoint<D, false, false>(P, q2[0], v2[0], obs, w[0]);
+                eval_waypoint<D, false, false>(P, q2[1], v2[1], obs, w[1]);
+                potential_pair<D>(P, obs, w[0], w[1]);
+            }
+        }
 #pragma unroll
         for (int j = 0; j < WPL; ++j) {
-            if (vl[j]) eval_waypoint<D>(P, q2[j], v2[j], obs, w[j], oreg);  // oreg: read only when nq == 3
+            if (WPL == 1 && vl[j]) eval_waypoint<D>(P, q2[j], v2[j], obs, w[j], oreg);  // oreg: read only when nq == 3
             cvs[j] = w[j].cv;
             const float u = P.one_m_lmax * (w[j].cv * P.invN) + ljl_e * ((w[j].jp + w[j].jv) * P.invN);
             if (j == 0) {
