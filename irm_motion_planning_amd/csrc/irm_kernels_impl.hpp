@@ -2050,22 +2050,45 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         }
         return __ballot(bfar) != 0ull;
     };
-    auto stage1 = [&](bool full) {  // Ypart[sp] = Fᵀ·[a'; b'] over this wave's unit
+    // GD single loop, fixed-shape launches: stage 1's B operand (both halves; the velocity half is used
+    // in dense rounds only) is read at the top of the round, before the flag word (X was written before
+    // the previous barrier), so the flag and operand LDS round trips overlap; same values, same MFMA
+    // order (bit-identical, tools/sched_check.py).  C3 0.769 -> 0.759 ms; the position half alone: no gain.
+    constexpr bool kFix1 = S::KQU > 0 && S::KQU <= S1Q;
+    constexpr int KQU1 = kFix1 ? S::KQU : S1Q;
+    // (the GD dual loop with the same prefetch: 4.33 -> 4.47 ms, 242 VGPRs there; not used)
+    constexpr bool kPre1 = GD1 && FULL && kFix1;
+    constexpr bool kPreW = kPre1 && RV;
+    auto stage1_load = [&](f32x4 (&bv)[KQU1], f32x4 (&bw)[KQU1]) {
+        const float* xl = X + cl * ldx + r4x;
+        if (has1) {  // wave-uniform
+#pragma unroll
+            for (int i = 0; i < KQU1; ++i) {
+                bv[i] = *reinterpret_cast<const f32x4*>(xl + (kq0 + i) * 16);
+                if constexpr (kPreW) bw[i] = *reinterpret_cast<const f32x4*>(xl + (KQa + kq0 + i) * 16);
+            }
+        }
+    };
+    auto stage1 = [&](bool full, const f32x4 (&pre)[KQU1], const f32x4 (&prew)[KQU1]) {  // Ypart[sp] = Fᵀ·[a'; b'] over this wave's unit
         if (!has1) return;
         const float* xl = X + cl * ldx + r4x;
-        constexpr bool kFix = S::KQU > 0 && S::KQU <= S1Q;
-        constexpr int KQU = kFix ? S::KQU : S1Q;
+        constexpr bool kFix = kFix1;
+        constexpr int KQU = KQU1;
         auto in = [&](int i) { return kFix ? i < KQU : kq0 + i < kq1; };
         const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
         f32x4 bv[KQU], bw[RV ? KQU : 1];
 #pragma unroll
-        for (int i = 0; i < KQU; ++i)
-            bv[i] = in(i) ? *reinterpret_cast<const f32x4*>(xl + (kq0 + i) * 16) : z4;
+        for (int i = 0; i < KQU; ++i) {
+            if constexpr (kPre1) bv[i] = pre[i];
+            else bv[i] = in(i) ? *reinterpret_cast<const f32x4*>(xl + (kq0 + i) * 16) : z4;
+        }
         if constexpr (RV) {
             if (full) {
 #pragma unroll
-                for (int i = 0; i < KQU; ++i)
-                    bw[i] = in(i) ? *reinterpret_cast<const f32x4*>(xl + (KQa + kq0 + i) * 16) : z4;
+                for (int i = 0; i < KQU; ++i) {
+                    if constexpr (kPreW) bw[i] = prew[i];
+                    else bw[i] = in(i) ? *reinterpret_cast<const f32x4*>(xl + (KQa + kq0 + i) * 16) : z4;
+                }
             }
         }
         f32x4 acc0 = z4, acc1 = z4;
@@ -2365,6 +2388,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // SIMD, item 4): C3 +1.7 %.  Priority only reorders issue: results are unchanged.
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
     for (int par = 0;; par ^= 1) {
+        f32x4 pre1[KQU1], pre1w[KQU1];
+        if constexpr (kPre1) stage1_load(pre1, pre1w);
         const unsigned fl = fw[par];
         if constexpr (GD1) {
             if ((fl & 0x7FFFFFFFu) == 0u) break;  // every trajectory of the block is done
@@ -2386,7 +2411,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         IRM_STAMP(0);
         if (dirr) {  // block-uniform
             IRM_COUNT(13, dense);
-            stage1(dense);
+            stage1(dense, pre1, pre1w);
             stage1z();
             IRM_STAMP(1);
             __syncthreads();
