@@ -98,7 +98,7 @@ def make_args(cfg, faithful, max_inner):
     return irm_main.parse_args(argv)
 
 
-def flops_per_iteration(N, D, O, R, split=False, lean=True):
+def flops_per_iteration(N, D, O, R, split=False, lean=True, ranks=None):
     """Algorithmic fp32 flops of one GD iteration of one trajectory.
 
     exec: what the optimiser kernel (waypoint-space rank-R iteration with the reference's fp32 α
@@ -113,7 +113,7 @@ def flops_per_iteration(N, D, O, R, split=False, lean=True):
     stages, the mixes, the α update of the accepted step) and one evaluation per line-search trial
     (waypoint update, obstacle pairs, FK / Jacobian / penalties); GD = one of each.
     """
-    Rz, Rf, Rg = (16, 16, 24) if (lean and R == 32) else (R, R, R)
+    Rz, Rf, Rg = ranks if ranks is not None else ((16, 16, 24) if (lean and R == 32) else (R, R, R))
     dir_f = 2 * R * N * D + 2 * Rz * N * D + 4 * Rf * N * D + 2 * Rg * N * D + 8 * N * D * D + 14 * N * D
     trial_f = 4 * N * D + 14 * N * O + 24 * N * D
     ref_f = 12 * N * N * D + 10 * N * D * D + 22 * N * O
@@ -122,31 +122,13 @@ def flops_per_iteration(N, D, O, R, split=False, lean=True):
     return dir_f + trial_f, ref_f
 
 
-def effective_tb(a, info, B):
-    """Trajectories per workgroup of the launch (choose_shape: info's traj_per_block is the shape's
-    maximum, an explicit --tb is capped by it)."""
-    return min(a.tb, info["traj_per_block"]) if a.tb else min(info["traj_per_block"], -(-B // info["num_cus"]))
-
-
-def optimiser_kernel(a, info, N, D, opt, B):
-    """Which optimiser kernel the launch uses (mirrors choose_shape / launch_optimize_shape)."""
-    tb = effective_tb(a, info, B)
-    nw = -(-N // 64) * 64
-    nk = -(-N // 16) * 16
-    nsplit = (nk // 16 + 3) // 4
-    bt = tb * nw
-    if 2 * -(-B // tb) <= info["num_cus"] and bt < 512:
-        bt = 512  # small batch: workgroup padded with trajectory-less waves (IRM_PAD_WAVES)
-    if bt < 512:  # lean kernel: at least one wave per stage-1 unit, 256- or 512-thread workgroups
-        bt = max(bt, min(512, 64 * 2 * nsplit))
-        bt = 256 if bt <= 256 else 512
-    waves = bt // 64
-    wpl = 2 if (nw == 256 and 512 < bt <= 1024) else 1  # N = 256, > 2 trajectories: 2 waypoints/lane
-    flow = "BLS dual loop" if opt == "bls" else ("GD dual loop" if a.faithful else "GD single loop")
-    lean = ((D, N) in ((3, 50), (3, 64), (3, 128), (3, 256), (7, 128), (7, 256)) and info["operator_rank"] == 32
-            and bt // wpl <= 512 and 2 * nsplit <= waves // wpl)
-    return (f"irm::k_lean ({flow}, {wpl} waypoint(s) per lane; fp32 MFMA 16x16x4 + VALU)" if lean
-            else "irm::k_optimize (fp32 MFMA 16x16x4 + VALU)")
+def plan_label(plan):
+    """Kernel label of the launch the library reports (irm_optimize_plan: filled in by its own launch
+    dispatch, so the label and the flop model's ranks are those of the kernel that runs)."""
+    flows = {0: "GD single loop", 1: "GD dual loop", 2: "BLS dual loop"}
+    return (f"irm::{plan['kernel']} ({flows[plan['flow']]}, {plan['waypoints_per_lane']} waypoint(s) per lane, "
+            f"{plan['traj_per_block']} trajectories per {plan['threads']}-thread workgroup, ranks z/dir/G "
+            f"{plan['rank_z']}/{plan['rank_dir']}/{plan['rank_g']}; fp32 MFMA 16x16x4 + VALU)")
 
 
 def cpu_baseline(cfg, args, start, goal, obstacles, budget_s=12.0):
@@ -198,7 +180,7 @@ def pmc_flops(cfg):
     return None, None
 
 
-def config_record(a, args, desc, B, N, D, O, opt, world, info):
+def config_record(a, args, desc, B, N, D, O, opt, world, info, plan=None):
     """The workload as run: shape, mode and every hyper-parameter that departs from main.py's defaults."""
     from irm_motion_planning_amd import main as irm_main
     defaults = vars(irm_main.parse_args([]))
@@ -214,7 +196,7 @@ def config_record(a, args, desc, B, N, D, O, opt, world, info):
         "gd_lr_first": float(args.gd_lr[0]),
         "overrides_vs_reference_defaults": overrides,
         "operator_rank": None if info is None else info["operator_rank"],
-        "traj_per_block": None if info is None else effective_tb(a, info, B),
+        "traj_per_block": None if plan is None else plan["traj_per_block"],
         "parallelism": f"dp{world} (batch sharded, env broadcast over {'gloo' if (a.dist_backend == 'gloo' or a.dry_run) else 'RCCL'})",
     }
 
@@ -382,8 +364,9 @@ def main():
     elapsed_max, iters_all = aggregate(elapsed, iters_rank, world, cdev)
     value = iters_all * a.steps / elapsed_max
 
-    kernel = optimiser_kernel(a, info, N, D, opt, B)
-    dir_f, trial_f, ref_f = flops_per_iteration(N, D, O, info["operator_rank"], split=True, lean="k_lean" in kernel)
+    plan = ctx.launch_plan(B, O)
+    kernel = plan_label(plan)
+    dir_f, trial_f, ref_f = flops_per_iteration(N, D, O, info["operator_rank"], split=True, ranks=(plan["rank_z"], plan["rank_dir"], plan["rank_g"]))
     exec_f = dir_f + trial_f
     # GD: one trial per iteration; BLS: the trials the line searches ran
     launch_flops = dir_f * iters_rank + trial_f * (trials_rank if opt == "bls" else iters_rank)
@@ -406,7 +389,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (SURVEY.md §8d seeds), reference environment",
-        "config": config_record(a, args, desc, B, N, D, O, opt, world, info),
+        "config": config_record(a, args, desc, B, N, D, O, opt, world, info, plan),
         "roofline": {
             # achieved = the flops one launch of THIS algorithm executes (the rank-R trajectory-space
             # GD iteration, DESIGN.md §5: exec_f per trajectory-iteration × the iterations of the

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define IRM_ABI_VERSION 2
+#define IRM_ABI_VERSION 3
 
 #define IRM_MAX_JOINTS 8       /* D  */
 #define IRM_MAX_TIMESTEPS 512  /* N  */
@@ -221,6 +221,33 @@ int irm_optimize_batch_dev(irm_ctx* ctx, const irm_batch_dev* args, void* stream
 
 /* Workspace sizing for irm_optimize_batch_dev callers that pass series_out. */
 int32_t irm_series_capacity(const irm_ctx* ctx);
+
+/* The optimiser launch that irm_optimize_batch(_dev) runs for `batch` problems with n_obstacles
+ * obstacles (record_series: series_out passed).  Filled in by the launch dispatch itself with
+ * nothing launched, so it names the kernel that actually runs (bench.py's flop model and kernel
+ * label come from here).  ABI 3; no reference counterpart. */
+typedef struct irm_launch_plan {
+    char kernel[128];           /* template instance, e.g. k_lean<FixShape<3,128,32>,512,1,FULL,GD1> */
+    int32_t lean;               /* 1: k_lean, 0: k_optimize                                */
+    int32_t flow;               /* 0 GD single loop, 1 GD dual loop, 2 BLS                 */
+    int32_t waypoints_per_lane;
+    int32_t threads;            /* per workgroup                                           */
+    int32_t grid;               /* workgroups                                              */
+    int32_t lds_bytes;          /* per workgroup                                           */
+    int32_t traj_per_block;
+    int32_t rank_z;             /* operator rank of the rounding-residual projection       */
+    int32_t rank_dir;           /* ... of the waypoint direction F·y''                     */
+    int32_t rank_g;             /* ... of the α-space gradient G = V_R·y''                 */
+    float lam16;                /* λ_16/λ_0 of [K; dK]ᵀ[K; dK] as built (0: not in the operator) */
+    float lam24;                /* λ_24/λ_0                                                */
+} irm_launch_plan;
+int irm_optimize_plan(const irm_ctx* ctx, int32_t batch, int32_t n_obstacles, int32_t record_series,
+                      irm_launch_plan* out);
+
+/* Source hash the library was built from: the first 16 hex digits of the SHA-256 over
+ * every file of irm_motion_planning_amd/csrc and include/irm.h (build.py); "unknown" otherwise.
+ * __graft_entry__.smoke() compares it with the checked-out sources.  ABI 3. */
+const char* irm_build_id(void);
 
 /* Diagnostics: per-workgroup phase cycle counters of the last optimize
  * launch (24 uint64 per workgroup).  Only a library built with

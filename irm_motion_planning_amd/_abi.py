@@ -11,7 +11,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("IRM_LIB") or os.path.join(HERE, "libirm_hip.so")
 
-IRM_ABI_VERSION = 2
+IRM_ABI_VERSION = 3
 IRM_MAX_JOINTS = 8
 IRM_MAX_TIMESTEPS = 512
 IRM_MAX_OBSTACLES = 64
@@ -100,6 +100,24 @@ class IrmInfo(ctypes.Structure):
     ]
 
 
+class IrmLaunchPlan(ctypes.Structure):
+    _fields_ = [
+        ("kernel", ctypes.c_char * 128),
+        ("lean", ctypes.c_int32),
+        ("flow", ctypes.c_int32),
+        ("waypoints_per_lane", ctypes.c_int32),
+        ("threads", ctypes.c_int32),
+        ("grid", ctypes.c_int32),
+        ("lds_bytes", ctypes.c_int32),
+        ("traj_per_block", ctypes.c_int32),
+        ("rank_z", ctypes.c_int32),
+        ("rank_dir", ctypes.c_int32),
+        ("rank_g", ctypes.c_int32),
+        ("lam16", ctypes.c_float),
+        ("lam24", ctypes.c_float),
+    ]
+
+
 class IrmBatchDev(ctypes.Structure):
     _fields_ = [
         ("alpha0", ctypes.c_void_p),
@@ -153,6 +171,10 @@ PROTOTYPES = {
     ),
     "irm_optimize_batch_dev": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(IrmBatchDev), ctypes.c_void_p]),
     "irm_series_capacity": (ctypes.c_int32, [ctypes.c_void_p]),
+    "irm_optimize_plan": (
+        ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(IrmLaunchPlan)]
+    ),
+    "irm_build_id": (ctypes.c_char_p, []),
     "irm_debug_phase_profile": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32]),
     "irm_debug_bls_trace_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32]),
     "irm_debug_bls_trace": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_int32]),

@@ -9,6 +9,8 @@ the objects build in parallel; the host-API kernels and dispatch
 lands next to this file so that it travels with the repository snapshot to the
 GPU box (it is git-ignored, not gpurun-ignored); objects stay in _obj/.
 """
+import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -44,9 +46,29 @@ ILP_SCHED = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
 LEAN_ILP_SHAPES = {(3, 256)}
 
 
+def source_files():
+    """Everything the library is compiled from (the build provenance hash covers exactly these)."""
+    return sorted(glob.glob(os.path.join(CSRC, "*"))) + [os.path.normpath(os.path.join(HERE, "..", "include", "irm.h"))]
+
+
+def source_hash():
+    """First 16 hex digits of the SHA-256 over the sources (names relative to the repo root, then
+    contents).  irm_build_id() of a library built here returns it (-DIRM_SOURCE_HASH on irm_host.cpp);
+    __graft_entry__.smoke() compares the two, so a stale prebuilt library fails."""
+    root = os.path.normpath(os.path.join(HERE, ".."))
+    h = hashlib.sha256()
+    for f in source_files():
+        h.update(os.path.relpath(f, root).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
 def units():
     """(object name, source, extra flags) of every compilation unit."""
-    u = [("irm_kernels", "irm_kernels.hip", []), ("irm_host", "irm_host.cpp", [])]
+    u = [("irm_kernels", "irm_kernels.hip", []),
+         ("irm_host", "irm_host.cpp", [f'-DIRM_SOURCE_HASH="{source_hash()}"'])]
     # (DynShape units keep the default scheduler: with iterative-ILP the D = 5 register-resident
     # variant, which spills heavily, left the exact-iteration band — tests/test_gpu_parity.py::
     # test_generic_shapes_match_reference_iteration[64-5] — so it is not used there)
@@ -76,6 +98,8 @@ def build(force=False, verbose=False, variant="", jobs=None):
         obj = os.path.join(odir, oname + ".o")
         objs.append(obj)
         deps = [os.path.join(CSRC, src), __file__] + HEADERS
+        if oname == "irm_host":  # carries the hash of every source
+            deps = deps + source_files()
         if force or _newer(obj, deps):
             todo.append([HIPCC] + CFLAGS + extra + flags + ["-c", "-o", obj, os.path.join(CSRC, src)])
 

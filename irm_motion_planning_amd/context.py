@@ -10,7 +10,7 @@ import ctypes
 import numpy as np
 
 from . import _abi
-from ._abi import IrmBatchDev, IrmInfo, IrmParams, IrmStats, check, load_library
+from ._abi import IrmBatchDev, IrmInfo, IrmLaunchPlan, IrmParams, IrmStats, check, load_library
 
 _fp = _abi.c_float_p
 
@@ -73,6 +73,15 @@ class Context:
         d = {name: getattr(inf, name) for name, _ in IrmInfo._fields_}
         d["device_name"] = d["device_name"].decode()
         d["arch"] = d["arch"].decode()
+        return d
+
+    def launch_plan(self, batch, n_obstacles=0, series=False):
+        """The optimiser launch optimize() runs for `batch` problems (irm_optimize_plan: filled in by
+        the library's own launch dispatch, nothing launched)."""
+        pl = IrmLaunchPlan()
+        check(self.lib.irm_optimize_plan(self._h, int(batch), int(n_obstacles), int(bool(series)), ctypes.byref(pl)))
+        d = {name: getattr(pl, name) for name, _ in IrmLaunchPlan._fields_}
+        d["kernel"] = d["kernel"].decode()
         return d
 
     def kernel_matrices(self):

@@ -240,6 +240,10 @@ struct irm_ctx {
     irm_params p{};
     int N = 0, D = 0, R = 0, NK = 0, MP = 0, RP = 0;
     float trunc = 0.f;
+    // λ_16/λ_0, λ_24/λ_0 of the operator actually built (0 where the component is not in it): the
+    // lean kernel's per-stage rank cuts (direction / residual at rank 16, G at rank 24) are exact to
+    // fp32 only while these are at fp32 noise, so they gate it (lean_rank_cut_ok)
+    float lam16 = 0.f, lam24 = 0.f;
     std::vector<float> t, cvec, K, dK, J;
     KParams kp{};
     // device
@@ -261,6 +265,11 @@ struct irm_ctx {
 };
 
 namespace {
+
+// Thresholds of the lean kernel's rank cuts on λ_r/λ_0 (see irm_ctx_create): the direction keeps its
+// terms to ≤ 1e-6 relative (fp32 rounding of the direction itself is 6e-8), G to σ_24/σ_0 ≤ 1e-7.
+constexpr float kLam16Max = 1e-6f, kLam24Max = 1e-14f;
+bool lean_rank_cut_ok(float lam16, float lam24) { return lam16 <= kLam16Max && lam24 <= kLam24Max; }
 
 int ensure_io(irm_ctx* c, size_t bytes) {
     if (bytes <= c->io_bytes) return 0;
@@ -521,6 +530,9 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
         }
         RP = round_up(R, 16);
         c->trunc = (R < N) ? (float)(std::max(0.0, G[(size_t)order[R] * N + order[R]]) / l0) : 0.f;
+        auto lam = [&](int r) { return (r < R) ? (float)(std::max(0.0, G[(size_t)order[r] * N + order[r]]) / l0) : 0.f; };
+        c->lam16 = lam(16);
+        c->lam24 = lam(24);
         Vd.assign((size_t)N * RP, 0.0);
         // Rank slot of component r.  At RP = 32 the second k-quad interleaves components 16-23 and
         // 24-31 so that the lean kernel's MFMAs 2 and 3 of that quad (k-permuted fragments: MFMA j
@@ -792,6 +804,11 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
     {
         const char* g = getenv("IRM_GENERAL_KERNEL");  // diagnostics: force the general optimiser
         kp.lean_ok = (g && g[0] == '1') ? 0 : 1;
+        // k_lean drops the components 16-31 from the waypoint direction (terms ∝ λ_r) and the residual
+        // projection, and 24-31 from G (∝ σ_r): only where those are at fp32 noise (σ = 0.1: λ16/λ0 ≈
+        // 1.5e-7, λ24/λ0 ≈ 6e-16).  A flatter spectrum (smaller --rbf-variance, e.g. 0.07: 4e-4 / 7e-9)
+        // still selects R = 32; it runs the general kernel at the full rank instead.
+        if (!lean_rank_cut_ok(c->lam16, c->lam24)) kp.lean_ok = 0;
         const char* w = getenv("IRM_LEAN_WPL");
         kp.lean_wpl = w ? atoi(w) : 0;
     }
@@ -1123,6 +1140,43 @@ int irm_optimize_batch_dev(irm_ctx* c, const irm_batch_dev* a, void* stream) {
 #endif
     HIP_TRY(irm::launch_optimize(kp, (hipStream_t)stream));
     return IRM_OK;
+}
+
+int irm_optimize_plan(const irm_ctx* c, int32_t batch, int32_t n_obstacles, int32_t record_series,
+                      irm_launch_plan* out) {
+    if (!c || !out || batch <= 0) return fail(IRM_EINVAL, "irm_optimize_plan: bad argument");
+    if (check_obs(n_obstacles)) return IRM_EINVAL;
+    memset(out, 0, sizeof(*out));
+    KParams kp = c->kp;
+    kp.B = batch;
+    kp.O = n_obstacles;
+    kp.record_series = record_series ? 1 : 0;
+    if (choose_shape(c, batch, true, kp, nullptr) <= 0) return fail(IRM_EINVAL, "no workgroup shape fits LDS");
+    irm::LaunchDesc d{};
+    d.describe_only = true;
+    HIP_TRY(irm::launch_optimize(kp, nullptr, &d));  // the dispatch fills d and launches nothing
+    snprintf(out->kernel, sizeof(out->kernel), "%s", d.kernel);
+    out->lean = d.lean;
+    out->flow = d.flow;
+    out->waypoints_per_lane = d.wpl;
+    out->threads = d.threads;
+    out->grid = d.grid;
+    out->lds_bytes = d.lds_bytes;
+    out->traj_per_block = d.traj_per_block;
+    out->rank_z = d.rank_z;
+    out->rank_dir = d.rank_dir;
+    out->rank_g = d.rank_g;
+    out->lam16 = c->lam16;
+    out->lam24 = c->lam24;
+    return IRM_OK;
+}
+
+const char* irm_build_id(void) {
+#ifdef IRM_SOURCE_HASH
+    return IRM_SOURCE_HASH;
+#else
+    return "unknown";
+#endif
 }
 
 int irm_optimize_batch(irm_ctx* c, const float* alpha0, const float* start, const float* goal, const float* obstacles,

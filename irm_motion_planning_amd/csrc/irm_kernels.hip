@@ -106,17 +106,17 @@ __global__ void k_init_alpha(KParams P, float* alpha_out) {
     alpha_out[e] = P.uvec[n] * sj + P.wvec[n] * gj;
 }
 
-hipError_t launch_optimize(const KParams& p, hipStream_t s) {
+hipError_t launch_optimize(const KParams& p, hipStream_t s, LaunchDesc* desc) {
     // shape-specialised kernels for the common configurations (auto rank R = 32)
     if (p.RP == 32 && p.nsplit == stage1_splits(p.NK) && !p.whole_robot) {
 #define IRM_TRY_FIX(D_, N_) \
-        if (p.D == D_ && p.N == N_) return launch_optimize_shape<FixShape<D_, N_, 32>>(p, s);
+        if (p.D == D_ && p.N == N_) return launch_optimize_shape<FixShape<D_, N_, 32>>(p, s, desc);
         IRM_FIX_SHAPES(IRM_TRY_FIX)
 #undef IRM_TRY_FIX
     }
     return dispatch_d(p.D, [&](auto dc) {
         constexpr int DD = decltype(dc)::value;
-        return launch_optimize_shape<DynShape<DD>>(p, s);
+        return launch_optimize_shape<DynShape<DD>>(p, s, desc);
     });
 }
 

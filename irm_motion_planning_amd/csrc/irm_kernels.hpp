@@ -276,9 +276,22 @@ inline bool regops_fit(const KParams& p) {
     return kq_per_unit <= s1q && tiles_per_wave <= s2t;
 }
 
+// What an optimiser launch runs, filled in by the launch dispatch itself (launch_optimize_shape), so
+// that irm_optimize_plan reports the kernel that a launch of the same arguments would run — not a
+// re-derivation of the dispatch rules.  describe_only: fill the record, launch nothing.
+struct LaunchDesc {
+    bool describe_only;
+    char kernel[128];  // template instance, e.g. "k_lean<FixShape<3,128,32>,512,1,FULL,GD1>"
+    int lean;          // 1: k_lean, 0: k_optimize
+    int flow;          // 0 GD single loop, 1 GD dual loop, 2 BLS (the lean kernel's LeanFlow)
+    int wpl;           // waypoints per lane
+    int threads, grid, lds_bytes, traj_per_block;
+    int rank_z, rank_dir, rank_g;  // operator rank of the residual projection, the waypoint direction, G
+};
+
 // launchers (return hipError_t)
 hipError_t launch_init_alpha(const KParams& p, float* alpha_out, hipStream_t s);
-hipError_t launch_optimize(const KParams& p, hipStream_t s);
+hipError_t launch_optimize(const KParams& p, hipStream_t s, LaunchDesc* desc = nullptr);
 hipError_t launch_forward(const KParams& p, int mode, hipStream_t s);  // mode: 0 evaluate, 1 cost, 2 cost+grad, 3 constraints
 hipError_t launch_fk(const KParams& p, const float* traj, float* pos, float* jac, hipStream_t s);
 hipError_t launch_fk_joints(const KParams& p, const float* traj, float* pos, hipStream_t s);

@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #include <type_traits>
 
@@ -2932,19 +2933,62 @@ inline bool lean_fits(const KParams& p) {
 // k_optimize<Shape> with the MAXT / operator-placement / optimiser variants (one shape per
 // instantiation unit, irm_opt_inst.hip).
 template <class Sh>
-hipError_t launch_general_shape(const KParams& p, hipStream_t s);
+hipError_t launch_general_shape(const KParams& p, hipStream_t s, LaunchDesc* desc);
+
+template <class Sh>
+inline int shape_name(char* buf, size_t n) {
+    if constexpr (Sh::kNW > 0) return snprintf(buf, n, "FixShape<%d,%d,%d>", Sh::D, Sh::N, Sh::RP);
+    else return snprintf(buf, n, "DynShape<%d>", Sh::D);
+}
+inline const char* flow_name(int flow) { return flow == LF_GD1 ? "GD1" : flow == LF_GD2 ? "GD2" : "BLS"; }
+// the optimiser's control flow in LeanFlow terms (k_optimize runs every flow in one instantiation)
+inline int optimizer_flow(const KParams& p) {
+    if (p.optimizer == IRM_OPT_BLS) return LF_BLS;
+    return (p.max_outer <= 1 && !p.record_series) ? LF_GD1 : LF_GD2;
+}
+
+// The one place an optimiser kernel is launched: records what runs in `desc` (irm_optimize_plan) and
+// launches unless desc->describe_only.
+template <class K>
+inline hipError_t run_optimizer(LaunchDesc* desc, K kernel, int grid, int threads, size_t lds, hipStream_t s,
+                                const KParams& p) {
+    if (desc) {
+        desc->grid = grid;
+        desc->threads = threads;
+        desc->lds_bytes = (int)lds;
+        desc->traj_per_block = p.TB;
+        if (desc->describe_only) return hipSuccess;
+    }
+    return launch_lds(kernel, grid, threads, lds, s, p);
+}
+
+template <class Sh, int TT, int WPL, bool FULL, int FLOW>
+hipError_t launch_lean_one(const KParams& p, int grid, hipStream_t s, LaunchDesc* desc) {
+    if (desc) {
+        char sn[48];
+        shape_name<Sh>(sn, sizeof(sn));
+        snprintf(desc->kernel, sizeof(desc->kernel), "k_lean<%s,%d,%d,%s,%s>", sn, TT, WPL, FULL ? "FULL" : "PART",
+                 flow_name(FLOW));
+        desc->lean = 1;
+        desc->flow = FLOW;
+        desc->wpl = WPL;
+        desc->rank_z = desc->rank_dir = 16;  // k_lean's per-stage ranks at RP = 32
+        desc->rank_g = 24;
+    }
+    return run_optimizer(desc, k_lean<Sh, TT, WPL, FULL, FLOW>, grid, p.BT, lean_lds(p), s, p);
+}
 
 template <class Sh, int TT, int WPL, bool FULL>
-hipError_t launch_lean_flow(const KParams& p, int flow, int grid, hipStream_t s) {
+hipError_t launch_lean_flow(const KParams& p, int flow, int grid, hipStream_t s, LaunchDesc* desc) {
     switch (flow) {
-        case LF_GD1: return launch_lds(k_lean<Sh, TT, WPL, FULL, LF_GD1>, grid, p.BT, lean_lds(p), s, p);
-        case LF_GD2: return launch_lds(k_lean<Sh, TT, WPL, FULL, LF_GD2>, grid, p.BT, lean_lds(p), s, p);
-        default: return launch_lds(k_lean<Sh, TT, WPL, FULL, LF_BLS>, grid, p.BT, lean_lds(p), s, p);
+        case LF_GD1: return launch_lean_one<Sh, TT, WPL, FULL, LF_GD1>(p, grid, s, desc);
+        case LF_GD2: return launch_lean_one<Sh, TT, WPL, FULL, LF_GD2>(p, grid, s, desc);
+        default: return launch_lean_one<Sh, TT, WPL, FULL, LF_BLS>(p, grid, s, desc);
     }
 }
 
 template <class Sh>
-hipError_t launch_optimize_shape(const KParams& p, hipStream_t s) {
+hipError_t launch_optimize_shape(const KParams& p, hipStream_t s, LaunchDesc* desc) {
     const int grid = (p.B + p.TB - 1) / p.TB;
     if (grid <= 0) return hipSuccess;
     return dispatch_t(p.BT, [&](auto tc) {
@@ -2957,12 +3001,12 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s) {
                 q.BT = p.BT / 2;
                 q.NW = p.NW / 2;
                 if (p.lean_wpl == 2 && flow == LF_GD1 && lean_fits(q))
-                    return launch_lds(k_lean<Sh, 256, 2>, grid, q.BT, lean_lds(q), s, q);
+                    return launch_lean_one<Sh, 256, 2, false, LF_GD1>(q, grid, s, desc);
             }
         }
         if constexpr (!Sh::kVariants && TT <= 512) {  // the lean kernel (F operators register-resident:
             // one stage-1 unit per wave; workgroups are padded to TT threads by choose_shape)
-            if (flow >= 0 && p.BT == TT && lean_fits(p)) return launch_lean_flow<Sh, TT, 1, true>(p, flow, grid, s);
+            if (flow >= 0 && p.BT == TT && lean_fits(p)) return launch_lean_flow<Sh, TT, 1, true>(p, flow, grid, s, desc);
         }
         if constexpr (!Sh::kVariants && TT == 1024) {
             if constexpr (Sh::kNW == 256 && Sh::D * 3 <= kCols) {  // ≥ 3 trajectories fit the MFMA columns
@@ -2970,10 +3014,10 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s) {
                 KParams q = p;
                 q.BT = p.BT / 2;
                 q.NW = p.NW / 2;
-                if (flow >= 0 && lean_fits(q)) return launch_lean_flow<Sh, 512, 2, false>(q, flow, grid, s);
+                if (flow >= 0 && lean_fits(q)) return launch_lean_flow<Sh, 512, 2, false>(q, flow, grid, s, desc);
             }
         }
-        return launch_general_shape<Sh>(p, s);
+        return launch_general_shape<Sh>(p, s, desc);
     });
 }
 
@@ -2982,7 +3026,7 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s) {
 // iterative-ILP machine scheduler, which measured 10 % faster on it (faithful C3) while the lean
 // kernels keep the default scheduler.
 template <class Sh>
-hipError_t launch_general_shape(const KParams& p, hipStream_t s) {
+hipError_t launch_general_shape(const KParams& p, hipStream_t s, LaunchDesc* desc) {
     const bool stage = p.ops_in_lds != 0;
     const Plan L = plan_lds(p, stage, true);
     const size_t lds = (size_t)L.total * 4;
@@ -2990,17 +3034,34 @@ hipError_t launch_general_shape(const KParams& p, hipStream_t s) {
     if (grid <= 0) return hipSuccess;
     return dispatch_t(p.BT, [&](auto tc) {
         constexpr int TT = decltype(tc)::value;
+        auto name = [&](bool ops_lds, bool regops, bool bls, bool full) {
+            if (!desc) return;
+            char sn[48];
+            shape_name<Sh>(sn, sizeof(sn));
+            snprintf(desc->kernel, sizeof(desc->kernel), "k_optimize<%s,%d,%s,%s,%s%s>", sn, TT,
+                     ops_lds ? "OPS_LDS" : "OPS_L2", regops ? "REGOPS" : "-", bls ? "BLS" : "GD", full ? ",FULL" : "");
+            desc->lean = 0;
+            desc->flow = optimizer_flow(p);
+            desc->wpl = 1;
+            desc->rank_z = desc->rank_dir = desc->rank_g = p.RP;
+        };
         auto go = [&](auto bc) {
             constexpr bool BB = decltype(bc)::value;
             if constexpr (TT <= 512) {
                 if constexpr (!Sh::kVariants) {
-                    if (p.regops && p.BT == TT)
-                        return launch_lds(k_optimize<Sh, TT, true, true, BB, true>, grid, p.BT, lds, s, p);
+                    if (p.regops && p.BT == TT) {
+                        name(true, true, BB, true);
+                        return run_optimizer(desc, k_optimize<Sh, TT, true, true, BB, true>, grid, p.BT, lds, s, p);
+                    }
                 }
-                if (p.regops) return launch_lds(k_optimize<Sh, TT, true, true, BB>, grid, p.BT, lds, s, p);
+                if (p.regops) {
+                    name(true, true, BB, false);
+                    return run_optimizer(desc, k_optimize<Sh, TT, true, true, BB>, grid, p.BT, lds, s, p);
+                }
             }
-            return stage ? launch_lds(k_optimize<Sh, TT, true, false, BB>, grid, p.BT, lds, s, p)
-                         : launch_lds(k_optimize<Sh, TT, false, false, BB>, grid, p.BT, lds, s, p);
+            name(stage, false, BB, false);
+            return stage ? run_optimizer(desc, k_optimize<Sh, TT, true, false, BB>, grid, p.BT, lds, s, p)
+                         : run_optimizer(desc, k_optimize<Sh, TT, false, false, BB>, grid, p.BT, lds, s, p);
         };
         return p.optimizer == IRM_OPT_BLS ? go(std::integral_constant<bool, true>{})
                                           : go(std::integral_constant<bool, false>{});
@@ -3021,9 +3082,10 @@ hipError_t launch_forward_dim(const KParams& p, int mode, hipStream_t s) {
 
 // Instantiated in irm_opt_inst.hip (IRM_INST_* macros); irm_kernels.hip only dispatches.
 #define IRM_FIX_SHAPES(X) X(3, 50) X(3, 64) X(3, 128) X(3, 256) X(7, 128) X(7, 256)
-#define IRM_EXTERN_FIX(D_, N_) extern template hipError_t launch_optimize_shape<FixShape<D_, N_, 32>>(const KParams&, hipStream_t);
-#define IRM_EXTERN_DYN(D_)                                                                          \
-    extern template hipError_t launch_optimize_shape<DynShape<D_>>(const KParams&, hipStream_t); \
+#define IRM_EXTERN_FIX(D_, N_) \
+    extern template hipError_t launch_optimize_shape<FixShape<D_, N_, 32>>(const KParams&, hipStream_t, LaunchDesc*);
+#define IRM_EXTERN_DYN(D_)                                                                                      \
+    extern template hipError_t launch_optimize_shape<DynShape<D_>>(const KParams&, hipStream_t, LaunchDesc*); \
     extern template hipError_t launch_forward_dim<D_>(const KParams&, int, hipStream_t);
 
 }  // namespace irm

@@ -8,15 +8,17 @@
 
 namespace irm {
 #if defined(IRM_INST_DYN)
-template hipError_t launch_general_shape<DynShape<IRM_INST_DYN>>(const KParams&, hipStream_t);
-template hipError_t launch_optimize_shape<DynShape<IRM_INST_DYN>>(const KParams&, hipStream_t);
+template hipError_t launch_general_shape<DynShape<IRM_INST_DYN>>(const KParams&, hipStream_t, LaunchDesc*);
+template hipError_t launch_optimize_shape<DynShape<IRM_INST_DYN>>(const KParams&, hipStream_t, LaunchDesc*);
 template hipError_t launch_forward_dim<IRM_INST_DYN>(const KParams&, int, hipStream_t);
 #elif defined(IRM_INST_FIX_D) && defined(IRM_INST_FIX_N)
 extern template hipError_t launch_general_shape<FixShape<IRM_INST_FIX_D, IRM_INST_FIX_N, 32>>(const KParams&,
-                                                                                               hipStream_t);
-template hipError_t launch_optimize_shape<FixShape<IRM_INST_FIX_D, IRM_INST_FIX_N, 32>>(const KParams&, hipStream_t);
+                                                                                               hipStream_t, LaunchDesc*);
+template hipError_t launch_optimize_shape<FixShape<IRM_INST_FIX_D, IRM_INST_FIX_N, 32>>(const KParams&, hipStream_t,
+                                                                                        LaunchDesc*);
 #elif defined(IRM_INST_GEN_D) && defined(IRM_INST_GEN_N)
-template hipError_t launch_general_shape<FixShape<IRM_INST_GEN_D, IRM_INST_GEN_N, 32>>(const KParams&, hipStream_t);
+template hipError_t launch_general_shape<FixShape<IRM_INST_GEN_D, IRM_INST_GEN_N, 32>>(const KParams&, hipStream_t,
+                                                                                       LaunchDesc*);
 #else
 #error "irm_opt_inst.hip needs IRM_INST_DYN, IRM_INST_FIX_D/N or IRM_INST_GEN_D/N"
 #endif

@@ -55,8 +55,9 @@ LAYOUT_C = r"""
 #include "irm.h"
 #define F(T, f) printf(#T " " #f " %zu\n", offsetof(T, f));
 int main(void) {
-  printf("sizeof irm_params %zu\nsizeof irm_stats %zu\nsizeof irm_info %zu\nsizeof irm_batch_dev %zu\n",
-         sizeof(irm_params), sizeof(irm_stats), sizeof(irm_info), sizeof(irm_batch_dev));
+  printf("sizeof irm_params %zu\nsizeof irm_stats %zu\nsizeof irm_info %zu\nsizeof irm_batch_dev %zu\n"
+         "sizeof irm_launch_plan %zu\n", sizeof(irm_params), sizeof(irm_stats), sizeof(irm_info),
+         sizeof(irm_batch_dev), sizeof(irm_launch_plan));
   %FIELDS%
   return 0;
 }
@@ -66,7 +67,7 @@ int main(void) {
 def test_struct_layout_matches_ctypes(tmp_path):
     from irm_motion_planning_amd import _abi
     structs = {"irm_params": _abi.IrmParams, "irm_stats": _abi.IrmStats, "irm_info": _abi.IrmInfo,
-               "irm_batch_dev": _abi.IrmBatchDev}
+               "irm_batch_dev": _abi.IrmBatchDev, "irm_launch_plan": _abi.IrmLaunchPlan}
     fields = "\n".join(f"F({cn}, {f})" for cn, cls in structs.items() for f, _ in cls._fields_)
     src = tmp_path / "layout.c"
     src.write_text(LAYOUT_C.replace("%FIELDS%", fields))
@@ -83,6 +84,13 @@ def test_struct_layout_matches_ctypes(tmp_path):
         assert got[("sizeof", cn)] == ctypes.sizeof(cls), cn
         for f, _ in cls._fields_:
             assert got[(cn, f)] == getattr(cls, f).offset, (cn, f)
+
+
+def test_build_id_is_the_source_hash(lib):
+    """The library names the sources it was built from (build.py embeds the hash); smoke() asserts
+    it equals the checked-out sources' hash, so a stale prebuilt library fails loudly."""
+    from irm_motion_planning_amd import build
+    assert lib.irm_build_id().decode() == build.source_hash()
 
 
 def test_params_default_equals_reference_argparse_defaults(lib):

@@ -336,7 +336,7 @@ def _oracle_band(o, a0, obs, s, g, n_ens=2):
     return T, st, spread, lspread
 
 
-def _bench_vs_ref(cfg, B, n_check, iters=200, lmax=None):
+def _bench_vs_ref(cfg, B, n_check, iters=200, lmax=None, argmod=None, operator_rank=0, want_kernel=None):
     """Bench mode (exactly `iters` GD steps per problem, k_lean) against the CPU oracle — the
     reference's fp32 α iteration with its rounding, pinned to the reference's own output at C3 / C4
     by tests/test_reference_bench.py — from the same α0 (the device's initTrajectory).
@@ -351,9 +351,13 @@ def _bench_vs_ref(cfg, B, n_check, iters=200, lmax=None):
     args = bench.make_args(cfg, False, iters)
     if lmax is not None:
         args.lambda_max_cost = lmax
+    if argmod is not None:
+        argmod(args)
     s, g, obs = bench.make_problem(cfg, 1, 0)
     s, g = s[:B], g[:B]
-    c = Context(params_from_args(args))
+    c = Context(params_from_args(args, operator_rank=operator_rank))
+    if want_kernel is not None:
+        assert c.launch_plan(B, len(obs))["kernel"].startswith(want_kernel), c.launch_plan(B, len(obs))
     alpha, traj, st = c.optimize(s, g, obs)
     assert np.all(st["grad_evals"] == iters) and np.all(np.isfinite(traj))
     o = Oracle(params_from_args(args))
@@ -399,6 +403,45 @@ def test_bench_c5_seven_dof():
 def test_bench_c7_seven_dof_n128():
     """north_star's target shape (7-DoF, 128 waypoints; FixShape<7, 128>, lean kernel)."""
     _bench_vs_ref("c7", 64, 4)
+
+
+@pytest.mark.parametrize("cfg,faithful,B,want", [
+    ("c3", False, 1024, "k_lean<FixShape<3,128,32>,512,1,FULL,GD1>"),
+    ("c3", True, 1024, "k_lean<FixShape<3,128,32>,512,1,FULL,GD2>"),
+    ("c3bls", False, 1024, "k_lean<FixShape<3,128,32>,512,1,FULL,BLS>"),
+    ("c4", False, 1024, "k_lean<FixShape<3,256,32>,512,2,PART,GD1>"),
+    ("c5", False, 512, "k_lean<FixShape<7,256,32>,512,1,FULL,GD1>"),
+    ("c7", False, 1024, "k_lean<FixShape<7,128,32>,256,1,FULL,GD1>"),
+    ("c2", True, 1, "k_lean<FixShape<3,128,32>,512,1,FULL,BLS>"),  # one trajectory, padded to 8 waves
+])
+def test_launch_plan_names_the_dispatched_kernel(cfg, faithful, B, want):
+    """irm_optimize_plan reports what the launch dispatch runs (bench.py's kernel label and flop
+    ranks come from it): the lean kernel with its per-stage ranks 16/16/24 at the bench configs."""
+    import bench
+    from irm_motion_planning_amd.context import Context
+    from irm_motion_planning_amd.params import params_from_args
+    c = Context(params_from_args(bench.make_args(cfg, faithful, 200)))
+    pl = c.launch_plan(B, bench.CONFIGS[cfg][4])
+    print(cfg, pl)
+    assert pl["kernel"] == want, pl
+    assert pl["grid"] * pl["traj_per_block"] >= B and (pl["grid"] - 1) * pl["traj_per_block"] < B
+    if pl["lean"]:
+        assert (pl["rank_z"], pl["rank_dir"], pl["rank_g"]) == (16, 16, 24)
+        assert pl["lam16"] < 1e-6 and pl["lam24"] < 1e-14
+    else:
+        assert pl["rank_z"] == pl["rank_dir"] == pl["rank_g"] == 32
+
+
+@pytest.mark.parametrize("sigma,rank", [(0.07, 0), (0.1, 32)])
+def test_rank_cuts_only_where_the_spectrum_allows(sigma, rank):
+    """k_lean drops singular components 16-31 (direction, residual) and 24-31 (G) of [K; dK]: exact to
+    fp32 at the default σ = 0.1 (λ16/λ0 ≈ 1.5e-7).  A flatter spectrum that still selects R = 32
+    (--rbf-variance 0.07: λ16/λ0 ≈ 4e-4) must run the general kernel at the full rank; both stay in the
+    oracle band (the oracle uses the dense operator), as does an explicit --operator-rank 32."""
+    def mod(a):
+        a.rbf_variance = sigma
+    want = "k_optimize" if sigma != 0.1 else "k_lean"
+    _bench_vs_ref("c3", 64, 3, iters=100, argmod=mod, operator_rank=rank, want_kernel=want)
 
 
 @pytest.mark.parametrize("cfg", ["c3", "c4", "c7"])
@@ -660,3 +703,128 @@ def test_generic_shapes_match_reference_iteration(N, D, links):
         print(f"N={N} D={D} b={b}: |traj - oracle| {err:.2e} (spread {spread:.2e}), loss {l_hip:.6f} vs {so['final_loss']:.6f}")
         assert err <= max(2.0 * spread, ORACLE_FLOOR), (b, err, spread)
         assert abs(l_hip - so["final_loss"]) <= 1e-3 * abs(so["final_loss"]) + 3 * lspread
+
+# ----------------------------------------------------------------- batched control flows (TB = 4)
+# The reference's own control flows as bench.py times them: the BLS dual loop (optimizer_BLS.py:127-213,
+# the reference's default optimiser; `bench.py --config c3bls`) and the GD dual loop
+# (optimizer_GD.py:173-232; `bench.py --config c3 --faithful`), four C3 trajectories sharing a 512-thread
+# k_lean workgroup's MFMA columns.
+
+FLOW_CFGS = [("c3bls", "BLS"), ("c3", "GD2")]
+
+
+def _flow_ctx(cfg, tb, faithful=True, iters=200):
+    import bench
+    from irm_motion_planning_amd.context import Context
+    from irm_motion_planning_amd.params import params_from_args
+    return Context(params_from_args(bench.make_args(cfg, faithful, iters), traj_per_block=tb))
+
+
+def _assert_same(x, y, what):
+    for u, v in zip(x, y):
+        if isinstance(u, dict):
+            for k in u:
+                np.testing.assert_array_equal(u[k], v[k], err_msg=f"{what}: {k}")
+        else:
+            np.testing.assert_array_equal(u, v, err_msg=what)
+
+
+@pytest.mark.parametrize("cfg,flow", FLOW_CFGS)
+@pytest.mark.parametrize("faithful", [True, False])
+def test_batched_flows_independent_of_workgroup_neighbours(cfg, flow, faithful):
+    """BLS / GD dual loop at four trajectories per workgroup (the instantiation the c3bls and C3
+    faithful bench lines time): α, trajectory and every statistic bit-identical under a permutation of
+    the batch, at 2 and 1 trajectories per workgroup, and for a problem solved alone.  (Bench mode of
+    the BLS flow = 200 fixed inner iterations, each with its line search; of GD = the dual-loop flow
+    is only used faithfully, so that case runs the GD single loop and is covered above.)"""
+    import bench
+    if flow == "GD2" and not faithful:
+        pytest.skip("GD bench mode runs the single-loop flow (test_result_independent_of_workgroup_neighbours)")
+    s, g, obs = bench.make_problem(cfg, 1, 0)
+    B = 64
+    s, g = s[:B], g[:B]
+    c4 = _flow_ctx(cfg, 4, faithful)
+    pl = c4.launch_plan(B, len(obs))
+    assert pl["kernel"] == f"k_lean<FixShape<3,128,32>,512,1,FULL,{flow}>" and pl["traj_per_block"] == 4, pl
+    ref = c4.optimize(s, g, obs)
+    assert np.all(np.isfinite(ref[1]))
+    perm = np.random.default_rng(5).permutation(B)
+    out = c4.optimize(s[perm], g[perm], obs)
+    _assert_same((out[0], out[1]), (ref[0][perm], ref[1][perm]), "permuted")
+    _assert_same((out[2],), ({k: v[perm] for k, v in ref[2].items()},), "permuted stats")
+    for tb in (2, 1):
+        c = _flow_ctx(cfg, tb, faithful)
+        assert c.launch_plan(B, len(obs))["kernel"].startswith("k_lean<FixShape<3,128,32>,512,1,FULL,")
+        _assert_same(c.optimize(s, g, obs), ref, f"tb={tb}")
+    c1 = _flow_ctx(cfg, 1, faithful)
+    for b in (0, 17, 63):
+        a1, t1, st1 = c1.optimize(s[b:b + 1], g[b:b + 1], obs)
+        _assert_same((a1[0], t1[0]), (ref[0][b], ref[1][b]), f"alone {b}")
+        _assert_same(({k: v[0] for k, v in st1.items()},), ({k: v[b] for k, v in ref[2].items()},), f"alone {b} stats")
+    print(f"{cfg} faithful={faithful}: grad evals mean {ref[2]['grad_evals'].mean():.1f} "
+          f"max {ref[2]['grad_evals'].max()}, trials {ref[2]['bls_trials'].sum()}")
+
+
+def test_batched_bls_line_search_follows_oracle():
+    """The BLS line search of three C3 problems, each traced while it shares a four-trajectory workgroup
+    (it is moved to batch index 0, which the line-search log records): the first 4 inner iterations
+    follow the oracle's from the same α0 trial for trial — accept / reject identical, lr exact — with
+    the losses, ‖g‖ and alpha_norm within the rank-32 operator's fp32 agreement (rtol below)."""
+    import bench
+    from conftest import oracle_for
+    from oracle.oracle import Oracle
+    from irm_motion_planning_amd.params import params_from_args
+    s, g, obs = bench.make_problem("c3bls", 1, 0)
+    B = 64
+    s, g = s[:B].copy(), g[:B].copy()
+    args = bench.make_args("c3bls", True, 200)
+    c = _flow_ctx("c3bls", 4)
+    c.bls_trace_enable(512)
+    o = Oracle(params_from_args(args))
+    worst = np.zeros(3)
+    for b in (5, 30, 47):
+        idx = np.arange(B)
+        idx[0], idx[b] = b, 0
+        _, _, st = c.optimize(s[idx], g[idx], obs)
+        tr = c.bls_trace(int(st["bls_trials"][0]))
+        _, so, tro = o.optimize_trace(c.init_alpha(s[b], g[b]), obs, s[b], g[b], cap=512)
+        sel = (tr[:, 0] == 0) & (tr[:, 1] < 4)
+        selo = (tro[:, 0] == 0) & (tro[:, 1] < 4)
+        a, r = tr[sel], tro[selo]
+        print(f"problem {b}: {len(a)} trials in the first 4 inner iterations, accepted {a[:, 6].astype(int).tolist()}")
+        assert len(a) == len(r) and len(a) >= 4, (b, len(a), len(r))
+        np.testing.assert_array_equal(a[:, 1:3], r[:, 1:3])  # inner iteration, trial index
+        np.testing.assert_array_equal(a[:, 6], r[:, 6])      # accept / reject
+        np.testing.assert_allclose(a[:, 3], r[:, 3], rtol=1e-7)  # lr
+        rel = lambda u, v: float(np.max(np.abs(u - v) / np.maximum(np.abs(v), 1e-30)))
+        worst = np.maximum(worst, [rel(a[:, 4], r[:, 4]), rel(a[:, 8], r[:, 8]), rel(a[:, 9], r[:, 9])])
+        np.testing.assert_allclose(a[:, 4], r[:, 4], rtol=1e-5)  # new_loss
+        np.testing.assert_allclose(a[:, 5], r[:, 5], rtol=1e-5)  # required_loss
+        np.testing.assert_allclose(a[:, 7], r[:, 7], rtol=1e-5)  # loss at α
+        np.testing.assert_allclose(a[:, 8], r[:, 8], rtol=1e-4)  # ‖g‖
+        np.testing.assert_allclose(a[:, 9], r[:, 9], rtol=1e-3)  # alpha_norm (a cancelling row sum)
+    print(f"largest relative differences: new_loss {worst[0]:.1e}, |g| {worst[1]:.1e}, alpha_norm {worst[2]:.1e}")
+
+
+@pytest.mark.parametrize("cfg", ["c3bls", "c3"])
+def test_batched_faithful_end_state_in_oracle_band(cfg):
+    """The reference control flow end to end at four trajectories per workgroup: for 4 problems of the
+    64-batch the final trajectory lies within max(2·spread, ORACLE_FLOOR) of the oracle's from the same
+    α0 (spread: the oracle's own change under ±1 ulp on α0 — large where the flow is chaotic), and the
+    constraint flag is one the oracle's runs produced."""
+    import bench
+    from oracle.oracle import Oracle
+    from irm_motion_planning_amd.params import params_from_args
+    s, g, obs = bench.make_problem(cfg, 1, 0)
+    B = 64
+    s, g = s[:B], g[:B]
+    c = _flow_ctx(cfg, 4)
+    _, traj, st = c.optimize(s, g, obs)
+    o = Oracle(params_from_args(bench.make_args(cfg, True, 200)))
+    for b in (0, 21, 42, 63):
+        a0 = c.init_alpha(s[b], g[b])
+        T, so, spread, _ = _oracle_band(o, a0, obs, s[b], g[b])
+        err = float(np.abs(traj[b] - T).max())
+        print(f"{cfg}[{b}] faithful: |traj - oracle| {err:.2e} (spread {spread:.2e}), grad evals "
+              f"{int(st['grad_evals'][b])} vs {so['grad_evals']}, ok {int(st['constraints_ok'][b])} vs {so['constraints_ok']}")
+        assert err <= max(2.0 * spread, ORACLE_FLOOR), (b, err, spread)

@@ -115,24 +115,18 @@ def test_bench_flop_model():
     assert gen_f == 10 * 32 * 128 * 3 + 8 * 128 * 9 + 42 * 128 * 3 + 14 * 128 * 11 == 167936
 
 
-def test_bench_kernel_label_mirrors_dispatch():
-    """bench.py names the optimiser kernel a launch uses (mirrors choose_shape / launch_optimize_shape):
-    the lean kernel for the specialised shapes in every control flow (GD single / dual loop, BLS up to
-    N = 128), the general one for other shapes, ranks and BLS at N = 256."""
-    import argparse
-
+def test_bench_kernel_label_is_the_library_plan():
+    """bench.py labels the kernel from irm_optimize_plan (the library's own dispatch; the GPU test
+    test_gpu_parity.py::test_launch_plan_names_the_dispatched_kernel checks the plans per config)."""
     import bench
-    info = {"traj_per_block": 5, "num_cus": 256, "operator_rank": 32}
-    for cfg, want in (("c3", "1 waypoint(s)"), ("c4", "2 waypoint(s)"), ("c5", "1 waypoint(s)"),
-                      ("c7", "1 waypoint(s)"), ("c2", "BLS dual loop")):
-        _, B, N, D, O, opt = bench.CONFIGS[cfg]
-        a = argparse.Namespace(tb=0, faithful=False)
-        i = dict(info, traj_per_block=16 // D)
-        assert want in bench.optimiser_kernel(a, i, N, D, opt, B), cfg
-    a = argparse.Namespace(tb=0, faithful=True)
-    assert "k_lean (GD dual loop" in bench.optimiser_kernel(a, info, 128, 3, "gd", 1024)
-    assert "k_lean (BLS dual loop, 2 waypoint" in bench.optimiser_kernel(a, info, 256, 3, "bls", 1024)
-    assert "k_optimize" in bench.optimiser_kernel(a, info, 100, 3, "gd", 1024)
+    plan = {"kernel": "k_lean<FixShape<3,128,32>,512,1,FULL,GD1>", "flow": 0, "waypoints_per_lane": 1,
+            "traj_per_block": 4, "threads": 512, "rank_z": 16, "rank_dir": 16, "rank_g": 24}
+    lab = bench.plan_label(plan)
+    assert lab.startswith("irm::k_lean<FixShape<3,128,32>,512,1,FULL,GD1> (GD single loop")
+    assert "4 trajectories per 512-thread workgroup" in lab and "16/16/24" in lab
+    f1, _ = bench.flops_per_iteration(128, 3, 11, 32, ranks=(16, 16, 24))
+    f2, _ = bench.flops_per_iteration(128, 3, 11, 32)
+    assert f1 == f2 == 124928
 
 
 def test_bench_args_bench_mode():
