@@ -131,11 +131,11 @@ def plan_label(plan):
             f"{plan['rank_z']}/{plan['rank_dir']}/{plan['rank_g']}; fp32 MFMA 16x16x4 + VALU)")
 
 
-def cpu_baseline(cfg, args, start, goal, obstacles, budget_s=12.0):
-    """Oracle (C restatement of the reference, OpenMP over trajectories) on a bounded sample."""
+def cpu_baseline_port(args, start, goal, obstacles, cores, budget_s=12.0):
+    """The scalar C oracle (restatement of the reference, fp64-accumulated contractions, OpenMP over
+    trajectories) on a bounded sample: full optimize() of each problem."""
     from irm_motion_planning_amd.params import params_from_args
     from oracle.oracle import Oracle
-    cores = max(1, min(16, len(os.sched_getaffinity(0))))
     p = params_from_args(args)
     orc = Oracle(p)
     t0 = time.perf_counter()
@@ -148,11 +148,52 @@ def cpu_baseline(cfg, args, start, goal, obstacles, budget_s=12.0):
     _, st = orc.optimize_batch(None, start[:n], goal[:n], obstacles, n_threads=cores)
     dt = time.perf_counter() - t0
     iters = sum(s["grad_evals"] for s in st)
-    return {"value": iters / dt, "unit": ("GD" if args.optimizer_name == "gd" else "BLS") + " iterations/s",
-            "cores": cores, "kind": "port",
-            "value_1thread": st1[0]["grad_evals"] / t1,  # 1-thread and all-cores rates
+    return {"value": iters / dt, "value_1thread": st1[0]["grad_evals"] / t1, "cores": cores,
+            "label": "scalar C oracle (oracle/irm_oracle.c), one problem per thread",
             "sample": f"{n} of the {len(start)} rank-0 problems, full optimize() each ({iters} iterations, "
                       f"{dt:.2f} s wall on {cores} threads); 1-thread rate {st1[0]['grad_evals'] / t1:.1f} it/s"}
+
+
+def cpu_baseline_batched(args, start, goal, obstacles, cores, budget_s=10.0):
+    """The vectorised fp32 restatement (oracle/batched_np.py): the whole sample's α as one N × (B·D)
+    matrix per worker, every contraction an OpenBLAS sgemm as the reference's XLA path contracts,
+    one worker process per core (forked before this process touches the GPU).  GD bench mode only."""
+    from irm_motion_planning_amd.params import params_from_args
+    from oracle import batched_np
+    from oracle.oracle import Oracle
+    if args.optimizer_name != "gd" or args.max_outer_iteration > 1 or args.loop_loss_reduction > -1e29:
+        return None  # the batched restatement runs the GD single loop with every step accepted
+    p = params_from_args(args)
+    orc = Oracle(p)
+    _, K, dK, J = orc.kernel_matrices()
+    iters = int(args.max_inner_iteration)
+    a0 = np.stack([orc.init_alpha(start[b], goal[b]) for b in range(len(start))])
+    # calibrate on one core, then size the sample to the budget
+    _, _, w = batched_np.run_processes(K, dK, J, p, a0[:16], start[:16], goal[:16], obstacles, 4, 1)
+    rate1 = 16 * 4 / w
+    n = int(min(len(start), max(cores, budget_s * rate1 * cores / iters)))
+    n = max(cores, (n // cores) * cores) if n >= cores else n
+    t0 = time.perf_counter()
+    _, _, wmax = batched_np.run_processes(K, dK, J, p, a0[:n], start[:n], goal[:n], obstacles, iters, cores)
+    wall = time.perf_counter() - t0
+    return {"value": n * iters / wmax, "value_1core": rate1, "cores": cores,
+            "label": "vectorised fp32 batch (oracle/batched_np.py): numpy + OpenBLAS sgemm over N x (B*D), "
+                     "one process per core",
+            "sample": f"{n} of the {len(start)} rank-0 problems x {iters} GD iterations, split over {cores} "
+                      f"processes ({wmax:.2f} s in the slowest, {wall:.2f} s wall incl. start-up); "
+                      f"1-core rate {rate1:.1f} it/s"}
+
+
+def cpu_baseline(cfg, args, start, goal, obstacles):
+    """Both CPU restatements timed on this host (rank 0's shard); `value` is the faster one."""
+    cores = max(1, min(16, len(os.sched_getaffinity(0))))
+    port = cpu_baseline_port(args, start, goal, obstacles, cores)
+    batched = cpu_baseline_batched(args, start, goal, obstacles, cores)
+    best = port if batched is None or port["value"] >= batched["value"] else batched
+    return {"value": best["value"], "unit": ("GD" if args.optimizer_name == "gd" else "BLS") + " iterations/s",
+            "cores": cores, "kind": "port", "sample": best["label"] + ": " + best["sample"],
+            "value_1thread": port["value_1thread"],  # SURVEY.md §8d: 1-thread and all-cores rates
+            "variants": {"scalar_oracle": port, "batched_fp32_numpy": batched}}
 
 
 def pmc_traffic(cfg):
@@ -311,6 +352,12 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if a.dry_run:
         return dry_run(a, world, rank)
+    desc, B, N, D, O, opt = CONFIGS[a.config]
+    args = make_args(a.config, a.faithful, a.max_inner)
+    start, goal, obstacles = make_problem(a.config, world, rank)
+    # the CPU baselines run first, before this process touches the GPU (the batched one forks workers)
+    cpu = cpu_baseline(a.config, args, start, goal, obstacles) if rank == 0 and not a.no_cpu_baseline else None
+
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     cdev = torch.device("cpu") if gloo else dev  # where the collectives' tensors live
@@ -318,10 +365,6 @@ def main():
     from irm_motion_planning_amd.context import Context, batch_dev
     from irm_motion_planning_amd._abi import IrmStats
     from irm_motion_planning_amd.params import params_from_args
-
-    desc, B, N, D, O, opt = CONFIGS[a.config]
-    args = make_args(a.config, a.faithful, a.max_inner)
-    start, goal, obstacles = make_problem(a.config, world, rank)
 
     # shared environment: rank 0's obstacles broadcast over RCCL/xGMI
     obs_t = share_environment(torch.from_numpy(obstacles).to(cdev), world).to(dev)
@@ -421,11 +464,9 @@ def main():
             "hbm_achieved_gbs": bytes_launch / (kernel_ms * 1e-3) / 1e9,
             "hbm_frac": bytes_launch / (kernel_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
         },
-        "cpu_baseline": None,
+        "cpu_baseline": cpu,  # rank 0's host cores, its own shard, every world size
         "iterations_per_step": iters_all,
     }
-    if rank == 0 and not a.no_cpu_baseline:  # rank 0's host cores, its own shard, every world size
-        result["cpu_baseline"] = cpu_baseline(a.config, args, start, goal, obstacles)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -692,10 +692,14 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
     kp.eps_v = p->eps_velocity;
     kp.lmax = p->lambda_max_cost;
     kp.lreg = p->lambda_reg;
-    // GD weight decay (1 − λ_reg·lr) per outer iteration: Python floats, cast to fp32 where they
-    // meet α (optimizer_GD.py:81, :185)
-    for (int i = 0; i < IRM_MAX_LR; ++i)
-        kp.gd_c[i] = (float)(1.0 - decimal_double(p->lambda_reg) * decimal_double(p->gd_lr[i]));
+    // GD weight decay (1 − λ_reg·lr) per outer iteration, in fp32 as the reference evaluates it:
+    // lr = dual_lr[k] is an fp32 array element (optimizer_GD.py:38-39, :209) and the Python float
+    // λ_reg enters weakly typed, so both the product and the difference round to fp32
+    // (optimizer_GD.py:81, :185) — two statements, so that the host compiler cannot fuse them
+    for (int i = 0; i < IRM_MAX_LR; ++i) {
+        const float prod = p->lambda_reg * p->gd_lr[i];
+        kp.gd_c[i] = 1.f - prod;
+    }
     kp.bls_lr0 = p->bls_lr_start;
     kp.bls_a = p->bls_alpha;
     kp.bls_bp = p->bls_beta_plus;
@@ -811,6 +815,10 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
         if (!lean_rank_cut_ok(c->lam16, c->lam24)) kp.lean_ok = 0;
         const char* w = getenv("IRM_LEAN_WPL");
         kp.lean_wpl = w ? atoi(w) : 0;
+        const char* sg = getenv("IRM_STAGGER");  // diagnostics: 1 odd workgroups, 2 the second half
+        kp.stagger = sg ? atoi(sg) : 0;
+        const char* sc = getenv("IRM_STAGGER_CYC");
+        kp.stagger_cyc = sc ? atoi(sc) : 4000;
     }
     c->max_series = p->max_series > 0 ? p->max_series : 1 + p->max_outer_iteration * p->max_inner_iteration;
     kp.max_series = c->max_series;

@@ -42,6 +42,7 @@ struct KParams {
     int32_t optimizer, max_inner, max_outer, max_bls, cvdl, record_series, max_series;
     int32_t lean_ok;  // k_gd_single may serve GD single-loop launches (IRM_GENERAL_KERNEL=1 clears it)
     int32_t lean_wpl; // diagnostics: IRM_LEAN_WPL=2 forces two waypoints per lane at N ≤ 128
+    int32_t stagger, stagger_cyc;  // diagnostics (IRM_STAGGER): delay half the workgroups' loop start
     float llr, lci, lsg0, ljl0, eps_p, eps_v, lmax, lreg;
     float bls_lr0, bls_a, bls_bp, bls_bm, vmax, pmax, pmin, pad1;
     // derived fp32 constants (reference casts its Python doubles to fp32)
@@ -258,9 +259,10 @@ __host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, in
     e.total = off;
     return e;
 }
-// V_R fragments staged in LDS for the lean kernel: N ≤ 128 at D ≤ 3 (C7's two 256-thread
-// workgroups per CU and every N = 256 shape read them from L2 instead: LDS budget)
-__host__ __device__ constexpr bool lean_vlds(int NK, int D) { return NK <= 128 && D <= 3; }
+// V_R fragments staged in LDS for the lean kernel: N ≤ 128 at D ≤ 3 in 512-thread workgroups (117 KiB
+// at N = 128).  256-thread workgroups run two per CU (76 KiB each without them) and every N = 256
+// shape reads them from L2 instead: LDS budget.
+__host__ __device__ constexpr bool lean_vlds(int NK, int D, int threads) { return NK <= 128 && D <= 3 && threads > 256; }
 
 // Stage-1 split-K factor: units of 4 k-quads over the position half.
 __host__ __device__ constexpr int stage1_splits(int NK) { return (NK / 16 + 3) / 4; }

@@ -1776,7 +1776,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     constexpr bool RV = MAXT > 256 || WPL > 1;  // velocity half of stage 1 register-resident too
     constexpr int NWL = S::NW / WPL;  // lanes per trajectory
     constexpr int WPTL = NWL / 64;    // waves per trajectory
-    constexpr bool VL = lean_vlds(S::NK, D);  // V_R fragments staged in LDS (else read from L2)
+    constexpr bool VL = lean_vlds(S::NK, D, MAXT);  // V_R fragments staged in LDS (else read from L2)
     static_assert(NWL % 64 == 0, "whole waves per trajectory");
     static_assert(WPL == 1 || (WPL == 2 && S::kNW > 0 && S::kNW == S::NK),
                   "two waypoints per lane: every lane's waypoints exist (N a multiple of 64)");
@@ -2388,6 +2388,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // the older one in every phase; static priority for that half (MI355X_MICROARCH.md, two waves per
     // SIMD, item 4): C3 +1.7 %.  Priority only reorders issue: results are unchanged.
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+    if (P.stagger) {  // diagnostics: start half the workgroups' rounds late (phase offset between co-resident ones)
+        const bool late = P.stagger == 1 ? (blockIdx.x & 1) != 0 : blockIdx.x >= (gridDim.x + 1) / 2;
+        if (late) {
+            const long long t0 = clock64();
+            while (clock64() - t0 < P.stagger_cyc) __builtin_amdgcn_s_sleep(2);
+        }
+    }
     for (int par = 0;; par ^= 1) {
         f32x4 pre1[KQU1], pre1w[KQU1];
         if constexpr (kPre1) stage1_load(pre1, pre1w);
@@ -2915,7 +2922,7 @@ struct type_tag {
 inline size_t lean_lds(const KParams& p) {
     KParams q = p;
     q.regops = 1;
-    return (size_t)lean_extra(plan_lds(q, false, true, true).total, p.MP, p.NK, p.RP, p.nsplit, lean_vlds(p.NK, p.D)).total * 4;
+    return (size_t)lean_extra(plan_lds(q, false, true, true).total, p.MP, p.NK, p.RP, p.nsplit, lean_vlds(p.NK, p.D, p.BT)).total * 4;
 }
 
 // The lean kernel's control flow for a launch (-1: the general kernel serves it): the GD single

@@ -1,4 +1,3 @@
-#include <stdio.h>
 /*
  * irm_oracle.c — plain-C fp32 restatement of the reference's α-space
  * optimiser.  TEST INFRASTRUCTURE ONLY (see irm_oracle.h).
@@ -12,10 +11,12 @@
 #include "irm_oracle.h"
 
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
+#endif
 
 /* A hyper-parameter the reference holds as a Python double (argparse) reaches this library as a
    float: recover the double the decimal argument denotes — the shortest decimal that round-trips the
@@ -29,7 +30,6 @@ static double decimal_double(float f) {
     }
     return (double)f;
 }
-#endif
 
 struct orc_ctx {
     irm_params p;
