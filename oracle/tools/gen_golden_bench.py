@@ -4,14 +4,16 @@ TEST INFRASTRUCTURE ONLY — runs in the build container, never on the GPU box. 
 imports the UNMODIFIED reference from /root/reference through oracle/tools/jaxshim (numpy adapter of
 the jax API; eager jit / while_loop / cond) and commits only generated arrays:
 
-  tests/golden/ref_bench_c3.npz   C3 (BASELINE configs[2]): 8 problems of bench.make_problem("c3"),
+  tests/golden/ref_bench_c3.npz   C3 (BASELINE configs[2]): 32 problems of bench.make_problem("c3"),
                                   N=128, the reference's 11 obstacles, GD single loop
                                   (optimizer_GD.py:68-97), bench mode (loop_loss_reduction=-1e30):
                                   α0, the 1..5-step trajectories and losses, the 200-step final
                                   trajectory and loss, and the same run from α0 ± 1 ulp (8 members)
                                   (trajectories as the reference evaluates them, K@α@J in fp32, and
                                   the fp32 α themselves, whose exact K@α@J the tests compare with)
-  tests/golden/ref_bench_c4.npz   the same at C4's shape (N=256, 50 random obstacles), 4 problems
+  tests/golden/ref_bench_c4.npz   the same at C4's shape (N=256, 50 random obstacles), 8 problems, with
+                                  the k-step iterates at k = 1..5, 10, 20, 50 (before the ±1-ulp
+                                  spread of this chaotic shape grows) and a 4-member ensemble
   tests/golden/ref_bls_trials.npz the first inner iterations of jit_optimize (optimizer_BLS.py:
                                   135-179): per iteration loss, ‖g‖, alpha_norm; per trial lr,
                                   new_loss, required_loss, accepted — at N=50 and N=128, from the
@@ -196,9 +198,10 @@ def main():
     os.makedirs(OUT, exist_ok=True)
 
     if "c3" in only:
-        np.savez_compressed(os.path.join(OUT, f"ref_bench_c3{sfx}.npz"), **gd_bench_fixture(refmain, ogd, "c3", 8, 8))
+        np.savez_compressed(os.path.join(OUT, f"ref_bench_c3{sfx}.npz"), **gd_bench_fixture(refmain, ogd, "c3", 32, 8))
     if "c4" in only:
-        np.savez_compressed(os.path.join(OUT, f"ref_bench_c4{sfx}.npz"), **gd_bench_fixture(refmain, ogd, "c4", 4, 4))
+        np.savez_compressed(os.path.join(OUT, f"ref_bench_c4{sfx}.npz"),
+                            **gd_bench_fixture(refmain, ogd, "c4", 8, 4, ks=(1, 2, 3, 4, 5, 10, 20, 50)))
     if "bls" in only:
         bl = {}
         for N in (50, 128):

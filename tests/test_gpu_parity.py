@@ -444,6 +444,33 @@ def test_rank_cuts_only_where_the_spectrum_allows(sigma, rank):
     _bench_vs_ref("c3", 64, 3, iters=100, argmod=mod, operator_rank=rank, want_kernel=want)
 
 
+@pytest.mark.parametrize("cfg", ["c5", "c3n256"])
+def test_dense_operator_at_n256(cfg):
+    """BASELINE configs[4]'s "dense RKHS Gram-matrix path cast to MFMA": --operator-rank -1 runs the
+    optimiser with F = [K; dK] itself (V = I, R = N = 256), i.e. the reference's dense K@α@J and
+    Kᵀ(…) + dKᵀ(…) contractions (trajectory.py:65, :295) on MFMA.  At C5's shape (7-DoF, N = 256) and
+    C3's problems at N = 256 (D = 3): 100 bench-mode GD steps inside the oracle band (as
+    test_bench_smooth_objective_tracks_oracle), and against the rank-32 default on the same problems —
+    the only independent check of the truncation at the 7-DoF shapes, which the reference (3 joints
+    hard-coded) cannot pin: |dense − rank 32| ≤ ORACLE_FLOOR, losses within 1e-3 relative."""
+    import bench
+    from irm_motion_planning_amd.context import Context
+    from irm_motion_planning_amd.params import params_from_args
+    B = 16
+    cd, _, td, std = _bench_vs_ref(cfg, B, 3, iters=100, operator_rank=-1, want_kernel="k_optimize")
+    assert cd.info()["operator_rank"] == 256 and cd.launch_plan(B, 11)["rank_dir"] == 256
+    args = bench.make_args(cfg, False, 100)
+    s, g, obs = bench.make_problem(cfg, 1, 0)
+    c32 = Context(params_from_args(args))
+    assert c32.info()["operator_rank"] == 32
+    _, t32, st32 = c32.optimize(s[:B], g[:B], obs, alpha0=cd.init_alpha(s[:B], g[:B]))
+    _, td0, std0 = cd.optimize(s[:B], g[:B], obs, alpha0=cd.init_alpha(s[:B], g[:B]))
+    err = np.abs(td0 - t32).reshape(B, -1).max(axis=1)
+    rel = np.abs(std0["final_loss"] - st32["final_loss"]) / np.abs(std0["final_loss"])
+    print(f"{cfg}: |dense - rank 32| max {err.max():.2e} median {np.median(err):.2e}, loss rel max {rel.max():.2e}")
+    assert err.max() <= ORACLE_FLOOR and rel.max() <= 1e-3
+
+
 @pytest.mark.parametrize("cfg", ["c3", "c4", "c7"])
 def test_result_independent_of_workgroup_neighbours(cfg):
     """Several trajectories share a workgroup (their MFMA columns) and a round runs the dense

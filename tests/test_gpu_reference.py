@@ -4,8 +4,9 @@ Same fixtures and tolerances as tests/test_reference_bench.py (which pins the CP
 tests/golden/ref_bench_c3.npz / ref_bench_c4.npz / ref_bls_trials.npz / ref_e2e_r02.npz, written by
 oracle/tools/gen_golden_bench.py from the unmodified reference.
 
-  * C3 (BASELINE configs[2]: N=128, the reference's 11 obstacles) and C4 (N=256, 50 random
-    obstacles), GD single loop in bench mode from the reference's α0: k ≤ 5 steps within
+  * C3 (BASELINE configs[2]: N=128, the reference's 11 obstacles; 32 problems) and C4 (N=256, 50
+    random obstacles; 8 problems), GD single loop in bench mode from the reference's α0, against the
+    reference with its own fp32 BLAS matmuls: k = 1..5 (C4 also 10, 20, 50) steps within
     max(2·spread_k, 1e-3) (SURVEY.md §8c's 1e-3, widened to the reference's own ±1-ulp sensitivity
     after k steps), loss rtol 1e-3; 200 steps within max(2·spread, 3e-3) of the reference's
     trajectory and the final loss inside the reference ensemble's range ± 1e-3 relative.  k_lean
@@ -22,8 +23,8 @@ import numpy as np
 import pytest
 
 from conftest import GOAL, START, check_iterations, check_quality, golden, params
-from test_reference_bench import (BENCH_ARGS, BLS_CASES, BLS_LOG_ARGS, E2E_R02, bench_band, check_bls_log, e2e_alpha0,
-                                  e2e_obstacles)
+from test_reference_bench import (BENCH_ARGS, BLS_CASES, BLS_LOG_ARGS, E2E_R02, bench_band, check_bls_log,
+                                  check_first_steps, e2e_alpha0, e2e_obstacles, loss_band)
 
 pytestmark = pytest.mark.gpu
 
@@ -40,15 +41,8 @@ def ctx(*argv, **overrides):
 
 @pytest.fixture(scope="module")
 def fx():
-    names = ("ref_bench_c3", "ref_bench_c3_xm", "ref_bench_c4", "ref_bench_c4_xm", "ref_bls_trials", "ref_e2e_r02")
+    names = ("ref_bench_c3", "ref_bench_c4", "ref_bls_trials", "ref_e2e_r02")
     return {name: golden(name) for name in names}
-
-
-def _variants(fx, cfg):
-    """The reference run with its fp32 BLAS matmuls and with correctly rounded matmuls (the
-    contraction arithmetic of this build; gen_golden_bench.py --matmul exact): the reference's
-    own result moves with that rounding, so the HIP result must sit in the band of one of them."""
-    return [("blas", fx["ref_bench_" + cfg]), ("xm", fx["ref_bench_" + cfg + "_xm"])]
 
 
 def _exact(c, alpha):
@@ -59,23 +53,34 @@ def _exact(c, alpha):
 
 @pytest.mark.parametrize("cfg", ["c3", "c4"])
 def test_gd_first_steps_match_reference(fx, cfg):
+    """The k-step GD iterates (C3: k = 1..5 on 32 problems; C4: k = 1..5, 10, 20, 50 on 8 problems)
+    against the reference run with its own fp32 BLAS matmuls (test_reference_bench.check_first_steps):
+    |traj − ref| ≤ max(2·spread_k, 1e-3) with spread_k the reference's own change after k steps under
+    ±1 ulp on α0 — except at an argmax knife edge of the max-cost term (two waypoint potentials within
+    the reference's K@α0 noise), where the result must match the reference re-run with correctly rounded
+    matmuls instead; loss within max(1e-3 relative, 3·its ±1-ulp change).  The widest band used is
+    printed."""
+    from conftest import oracle_for
     z = fx["ref_bench_" + cfg]
+    zx = golden("ref_bench_" + cfg + "_xm")
     N = int(z["traj_final"].shape[1])
+    widest, edges = 0.0, []
     for i, k in enumerate(z["ks"]):
         c = ctx(*BENCH_ARGS, "--n-timesteps", N, "--max-inner-iteration", int(k))
+        o = oracle_for(*BENCH_ARGS, "--n-timesteps", N, "--max-inner-iteration", int(k))
         alpha, traj, st = c.optimize(z["start"], z["goal"], z["obstacles"], alpha0=z["alpha0"])
         assert np.all(st["grad_evals"] == k)
+        errs = []
         for b in range(len(z["start"])):
-            res = []
-            for name, zv in _variants(fx, cfg):
-                ref = _exact(c, zv["alpha_k"][b, i])
-                spread = max(float(np.abs(_exact(c, a) - ref).max()) for a in zv["ens_alpha_k"][b, :, i])
-                err = float(np.abs(traj[b] - ref).max())
-                res.append((err <= max(2.0 * spread, 1e-3), name, err, spread))
-            print(f"{cfg}[{b}] {k} steps: " + ", ".join(f"{n}: |traj - ref| {e:.2e} (spread {sp:.2e})"
-                                                         for _, n, e, sp in res))
-            assert any(r[0] for r in res), (cfg, k, b, res)
-            assert abs(float(st["final_loss"][b]) - z["loss_k"][b, i]) <= 1e-3 * abs(z["loss_k"][b, i])
+            zm, err, band, m = check_first_steps(o, z, zx, b, i, traj[b])
+            widest = max(widest, band)
+            errs.append(err)
+            if m is not None:
+                edges.append((int(k), b, m))
+            assert abs(float(st["final_loss"][b]) - zm["loss_k"][b, i]) <= loss_band(o, zm, b, i), (k, b)
+        print(f"{cfg} {k} steps: |traj - ref (BLAS)| max {max(errs):.2e} over {len(errs)} problems")
+    print(f"{cfg}: widest band used {widest:.2e}; argmax knife edges {edges}")
+    assert len(edges) <= 3
 
 
 @pytest.mark.parametrize("cfg", ["c3", "c4"])

@@ -11,10 +11,15 @@ unmodified reference (oracle/tools/gen_golden_bench.py through the jax adapter):
   * reference control flow end to end (GD λ_max table, N=128 / 256) with ±1-ulp ensembles.
 
 Tolerances (shared with the GPU tests in test_gpu_reference.py):
-  * k ≤ 5 GD steps: waypoints within max(2·spread_k, 1e-3) (SURVEY.md §8c's 1e-3, widened to the
+  * k-step GD iterates (C3 k = 1..5 on 32 problems; C4 k = 1..5, 10, 20, 50 on 8 problems) against the
+    reference with its own fp32 BLAS matmuls: waypoints within max(2·spread_k, 1e-3), loss within
+    max(1e-3 relative, 3·its ±1-ulp change) (SURVEY.md §8c's 1e-3, widened to the
     reference's own ±1-ulp sensitivity after k steps: at N=256 with 50 obstacles the fp32 noise of
     K@α0 moves the first gradient's max-cost argmax and one step already spreads 3.5e-3), loss rtol
     1e-3 (near α0 the reference's loss carries the fp32 noise of K@α0 in its start / goal terms);
+    the one exception is an argmax knife edge (ARGMAX_KNIFE_EDGE: two waypoint potentials within the
+    reference's own K@α0 noise — C3 problems 8 and 15), which must then match the reference re-run with
+    correctly rounded matmuls;
   * trajectories are compared as K·α·J of the reference's fp32 α in exact arithmetic (its own
     evaluate adds the fp32 noise of K@α with |α| ≈ 1e3 on top: 1.5e-3 at N=128, 7e-3 at N=256);
   * 200 GD steps: |traj − ref|∞ ≤ max(2·spread, 3e-3) with spread = the reference's own distance to its
@@ -71,20 +76,72 @@ def exact_traj(o, alpha):
     return np.asarray(K, np.float64) @ np.asarray(alpha, np.float64) @ np.asarray(J, np.float64)
 
 
+# The reference's max-cost term (λmax·max_n cost_v, trajectory.py:85-97) takes the first-index argmax of
+# the per-waypoint potential.  Where the two largest potentials are closer than the fp32 noise its BLAS
+# K@α0 carries (|α| ≈ 1e3: ~1e-4 relative in the potential), which waypoint is the maximum is decided by
+# that noise, and a correctly rounded evaluation may pick the other one.
+ARGMAX_KNIFE_EDGE = 2e-4
+
+
+def argmax_margin(o, z, b, i):
+    """Smallest relative gap between the two largest per-waypoint potentials (exact evaluation) over
+    the reference's iterates α0, α_k (k < ks[i]) of problem b."""
+    from oracle.oracle import compute_cost_vg
+    alphas = [z["alpha0"][b]] + [z["alpha_k"][b, j] for j in range(i)]
+    m = np.inf
+    for a in alphas:
+        cv, _ = compute_cost_vg(o.fk(o.evaluate(a)), z["obstacles"])
+        top = np.sort(cv)[::-1]
+        m = min(m, float((top[0] - top[1]) / top[0]))
+    return m
+
+
+def check_first_steps(o, z, zx, b, i, traj):
+    """k-step parity against the reference with its own fp32 BLAS matmuls (z): |traj − ref| ≤
+    max(2·spread_k, 1e-3).  The only accepted exception is the argmax knife edge above: then the result
+    must match the reference with correctly rounded matmuls (zx) in its band instead.  Returns
+    (the fixture matched, err vs BLAS, band, knife-edge margin or None)."""
+    ref = exact_traj(o, z["alpha_k"][b, i])
+    spread = max(float(np.abs(exact_traj(o, a) - ref).max()) for a in z["ens_alpha_k"][b, :, i])
+    err, band = float(np.abs(traj - ref).max()), max(2.0 * spread, 1e-3)
+    if err <= band:
+        return z, err, band, None
+    m = argmax_margin(o, z, b, i)
+    refx = exact_traj(o, zx["alpha_k"][b, i])
+    spx = max(float(np.abs(exact_traj(o, a) - refx).max()) for a in zx["ens_alpha_k"][b, :, i])
+    errx = float(np.abs(traj - refx).max())
+    assert m <= ARGMAX_KNIFE_EDGE and errx <= max(2.0 * spx, 1e-3), (int(z["ks"][i]), b, err, band, m, errx)
+    return zx, err, band, m
+
+
+def loss_band(o, z, b, i):
+    """Loss tolerance after k steps: 1e-3 relative, or 3× the reference's own loss change under ±1 ulp
+    on α0 after those k steps (its ensemble α_k, evaluated here) where that is larger (C4 at k ≥ 10)."""
+    p = o.params
+    lam = (p.lambda_sg_constraint, p.lambda_jl_constraint, p.lambda_max_cost)
+    c0 = o.cost(z["alpha_k"][b, i], z["obstacles"], z["start"][b], z["goal"][b], *lam)
+    ls = max(abs(o.cost(a, z["obstacles"], z["start"][b], z["goal"][b], *lam) - c0) for a in z["ens_alpha_k"][b, :, i])
+    return max(1e-3 * abs(float(z["loss_k"][b, i])), 3.0 * ls)
+
+
 @pytest.mark.parametrize("cfg", ["c3", "c4"])
 def test_oracle_gd_first_steps(cfg, g_c3, g_c4):
+    """C3: k = 1..5 on 32 problems; C4: k = 1..5, 10, 20, 50 on 8 problems (check_first_steps)."""
     z = g_c3 if cfg == "c3" else g_c4
+    zx = golden("ref_bench_" + cfg + "_xm")
     N = _n(z)
+    edges = []
     for i, k in enumerate(z["ks"]):
         o = oracle_for(*BENCH_ARGS, "--n-timesteps", N, "--max-inner-iteration", int(k))
         for b in range(len(z["start"])):
             al, st = o.optimize(z["alpha0"][b], z["obstacles"], z["start"][b], z["goal"][b])
             assert st["grad_evals"] == k
-            ref = exact_traj(o, z["alpha_k"][b, i])
-            spread = max(float(np.abs(exact_traj(o, a) - ref).max()) for a in z["ens_alpha_k"][b, :, i])
-            err = float(np.abs(o.evaluate(al) - ref).max())
-            assert err <= max(2.0 * spread, 1e-3), (cfg, k, b, err, spread)
-            assert abs(st["final_loss"] - z["loss_k"][b, i]) <= 1e-3 * abs(z["loss_k"][b, i])
+            zm, _, _, m = check_first_steps(o, z, zx, b, i, o.evaluate(al))
+            if m is not None:
+                edges.append((int(k), b, m))
+            assert abs(st["final_loss"] - zm["loss_k"][b, i]) <= loss_band(o, zm, b, i)
+    print(f"{cfg}: argmax knife edges {edges}")
+    assert len(edges) <= 3
 
 
 @pytest.mark.parametrize("cfg", ["c3", "c4"])
