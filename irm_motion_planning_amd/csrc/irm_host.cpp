@@ -817,6 +817,8 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
         kp.lean_wpl = w ? atoi(w) : 0;
         const char* sg = getenv("IRM_STAGGER");  // diagnostics: 1 odd workgroups, 2 the second half
         kp.stagger = sg ? atoi(sg) : 0;
+        const char* l2 = getenv("IRM_LEAN2");  // k_lean2 for the GD single loop at N = 128, D = 3
+        kp.lean2 = l2 ? atoi(l2) : 0;
         const char* sc = getenv("IRM_STAGGER_CYC");
         kp.stagger_cyc = sc ? atoi(sc) : 4000;
     }

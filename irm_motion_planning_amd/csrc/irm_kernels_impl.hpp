@@ -2793,6 +2793,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     if (tid == 0) prof.flush(P.prof);
 }
 
+#include "irm_lean2.hpp"
+
 // --------------------------------------------------- α-space eval kernels
 // mode 0: evaluate (K or dK)·α·J; 1: cost; 2: cost + grad; 3: constraints.
 // trajectory.py:63-65, 271-297, 129-180; same lane mapping as k_optimize.
@@ -3009,6 +3011,27 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s, LaunchDesc* de
                 q.NW = p.NW / 2;
                 if (p.lean_wpl == 2 && flow == LF_GD1 && lean_fits(q))
                     return launch_lean_one<Sh, 256, 2, false, LF_GD1>(q, grid, s, desc);
+            }
+        }
+        if constexpr (!Sh::kVariants && Sh::kNW == 128 && Sh::D == 3) {
+            // k_lean2: the GD single loop with two lanes per waypoint, 16 waves for up to 4 trajectories
+            if (p.lean2 && flow == LF_GD1 && p.TB <= 4) {
+                KParams q = p;
+                q.BT = 1024;
+                q.NW = 256;
+                if (lean2_lds(q) <= 160 * 1024) {
+                    if (desc) {
+                        char sn[48];
+                        shape_name<Sh>(sn, sizeof(sn));
+                        snprintf(desc->kernel, sizeof(desc->kernel), "k_lean2<%s,1024,LPW2,GD1>", sn);
+                        desc->lean = 1;
+                        desc->flow = LF_GD1;
+                        desc->wpl = 1;
+                        desc->rank_z = desc->rank_dir = 16;
+                        desc->rank_g = 24;
+                    }
+                    return run_optimizer(desc, k_lean2<Sh>, grid, 1024, lean2_lds(q), s, q);
+                }
             }
         }
         if constexpr (!Sh::kVariants && TT <= 512) {  // the lean kernel (F operators register-resident:

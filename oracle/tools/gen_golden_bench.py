@@ -13,7 +13,7 @@ the jax API; eager jit / while_loop / cond) and commits only generated arrays:
                                   the fp32 α themselves, whose exact K@α@J the tests compare with)
   tests/golden/ref_bench_c4.npz   the same at C4's shape (N=256, 50 random obstacles), 8 problems, with
                                   the k-step iterates at k = 1..5, 10, 20, 50 (before the ±1-ulp
-                                  spread of this chaotic shape grows) and a 4-member ensemble
+                                  spread of this chaotic shape grows) and an 8-member ensemble
   tests/golden/ref_bls_trials.npz the first inner iterations of jit_optimize (optimizer_BLS.py:
                                   135-179): per iteration loss, ‖g‖, alpha_norm; per trial lr,
                                   new_loss, required_loss, accepted — at N=50 and N=128, from the
@@ -201,7 +201,7 @@ def main():
         np.savez_compressed(os.path.join(OUT, f"ref_bench_c3{sfx}.npz"), **gd_bench_fixture(refmain, ogd, "c3", 32, 8))
     if "c4" in only:
         np.savez_compressed(os.path.join(OUT, f"ref_bench_c4{sfx}.npz"),
-                            **gd_bench_fixture(refmain, ogd, "c4", 8, 4, ks=(1, 2, 3, 4, 5, 10, 20, 50)))
+                            **gd_bench_fixture(refmain, ogd, "c4", 8, 8, ks=(1, 2, 3, 4, 5, 10, 20, 50)))
     if "bls" in only:
         bl = {}
         for N in (50, 128):

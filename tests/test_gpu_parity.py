@@ -444,31 +444,52 @@ def test_rank_cuts_only_where_the_spectrum_allows(sigma, rank):
     _bench_vs_ref("c3", 64, 3, iters=100, argmod=mod, operator_rank=rank, want_kernel=want)
 
 
+# At N = 256 the max-cost argmax is a near-tie at almost every problem (the two largest waypoint
+# potentials within 1e-5 - 2e-4 relative at α0, tools/dense_diag.py), so the oracle's ±1-ulp ensemble
+# under-samples the iteration's sensitivity there; measured after 100 C3-at-N=256 steps: dense and
+# rank-32 GPU runs within 1.6e-3 of each other and both 3e-4 - 9.6e-3 from the fp64-accumulating oracle.
+N256_ORACLE_FLOOR = 1.5e-2
+
+
 @pytest.mark.parametrize("cfg", ["c5", "c3n256"])
 def test_dense_operator_at_n256(cfg):
     """BASELINE configs[4]'s "dense RKHS Gram-matrix path cast to MFMA": --operator-rank -1 runs the
     optimiser with F = [K; dK] itself (V = I, R = N = 256), i.e. the reference's dense K@α@J and
     Kᵀ(…) + dKᵀ(…) contractions (trajectory.py:65, :295) on MFMA.  At C5's shape (7-DoF, N = 256) and
-    C3's problems at N = 256 (D = 3): 100 bench-mode GD steps inside the oracle band (as
-    test_bench_smooth_objective_tracks_oracle), and against the rank-32 default on the same problems —
-    the only independent check of the truncation at the 7-DoF shapes, which the reference (3 joints
-    hard-coded) cannot pin: |dense − rank 32| ≤ ORACLE_FLOOR, losses within 1e-3 relative."""
+    C3's problems at N = 256 (D = 3), 100 bench-mode GD steps on 16 problems from the same α0:
+      * against the rank-32 default — the only independent check of the truncation at the 7-DoF
+        shapes, which the reference (3 joints hard-coded) cannot pin: |dense − rank 32| ≤ ORACLE_FLOOR
+        on every problem, final losses within 1e-4 relative;
+      * against the oracle (fp64-accumulated α-space contractions) on every problem: final loss within
+        1e-3 relative, waypoints within max(2·spread, N256_ORACLE_FLOOR)."""
     import bench
     from irm_motion_planning_amd.context import Context
     from irm_motion_planning_amd.params import params_from_args
-    B = 16
-    cd, _, td, std = _bench_vs_ref(cfg, B, 3, iters=100, operator_rank=-1, want_kernel="k_optimize")
-    assert cd.info()["operator_rank"] == 256 and cd.launch_plan(B, 11)["rank_dir"] == 256
-    args = bench.make_args(cfg, False, 100)
+    from oracle.oracle import Oracle
+    B, iters = 16, 100
+    args = bench.make_args(cfg, False, iters)
     s, g, obs = bench.make_problem(cfg, 1, 0)
+    s, g = s[:B], g[:B]
+    cd = Context(params_from_args(args, operator_rank=-1))
     c32 = Context(params_from_args(args))
+    pl = cd.launch_plan(B, len(obs))
+    assert cd.info()["operator_rank"] == 256 and pl["rank_dir"] == 256 and pl["kernel"].startswith("k_optimize"), pl
     assert c32.info()["operator_rank"] == 32
-    _, t32, st32 = c32.optimize(s[:B], g[:B], obs, alpha0=cd.init_alpha(s[:B], g[:B]))
-    _, td0, std0 = cd.optimize(s[:B], g[:B], obs, alpha0=cd.init_alpha(s[:B], g[:B]))
-    err = np.abs(td0 - t32).reshape(B, -1).max(axis=1)
-    rel = np.abs(std0["final_loss"] - st32["final_loss"]) / np.abs(std0["final_loss"])
+    a0 = cd.init_alpha(s, g)
+    _, td, std = cd.optimize(s, g, obs, alpha0=a0)
+    _, t32, st32 = c32.optimize(s, g, obs, alpha0=a0)
+    assert np.all(std["grad_evals"] == iters) and np.all(st32["grad_evals"] == iters)
+    err = np.abs(td - t32).reshape(B, -1).max(axis=1)
+    rel = np.abs(std["final_loss"] - st32["final_loss"]) / np.abs(std["final_loss"])
     print(f"{cfg}: |dense - rank 32| max {err.max():.2e} median {np.median(err):.2e}, loss rel max {rel.max():.2e}")
-    assert err.max() <= ORACLE_FLOOR and rel.max() <= 1e-3
+    assert err.max() <= ORACLE_FLOOR and rel.max() <= 1e-4
+    o = Oracle(params_from_args(args))
+    for b in range(B):
+        T, so, spread, _ = _oracle_band(o, a0[b], obs, s[b], g[b], n_ens=1)
+        e = float(np.abs(td[b] - T).max())
+        lr_ = abs(float(std["final_loss"][b]) - so["final_loss"]) / abs(so["final_loss"])
+        print(f"  [{b}] dense - oracle {e:.2e} (spread {spread:.2e}), loss rel {lr_:.1e}")
+        assert e <= max(2.0 * spread, N256_ORACLE_FLOOR) and lr_ <= 1e-3, (b, e, spread, lr_)
 
 
 @pytest.mark.parametrize("cfg", ["c3", "c4", "c7"])
