@@ -815,12 +815,6 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
         if (!lean_rank_cut_ok(c->lam16, c->lam24)) kp.lean_ok = 0;
         const char* w = getenv("IRM_LEAN_WPL");
         kp.lean_wpl = w ? atoi(w) : 0;
-        const char* sg = getenv("IRM_STAGGER");  // diagnostics: 1 odd workgroups, 2 the second half
-        kp.stagger = sg ? atoi(sg) : 0;
-        const char* l2 = getenv("IRM_LEAN2");  // k_lean2 for the GD single loop at N = 128, D = 3
-        kp.lean2 = l2 ? atoi(l2) : 0;
-        const char* sc = getenv("IRM_STAGGER_CYC");
-        kp.stagger_cyc = sc ? atoi(sc) : 4000;
     }
     c->max_series = p->max_series > 0 ? p->max_series : 1 + p->max_outer_iteration * p->max_inner_iteration;
     kp.max_series = c->max_series;

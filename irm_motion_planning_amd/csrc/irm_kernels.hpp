@@ -42,8 +42,6 @@ struct KParams {
     int32_t optimizer, max_inner, max_outer, max_bls, cvdl, record_series, max_series;
     int32_t lean_ok;  // k_gd_single may serve GD single-loop launches (IRM_GENERAL_KERNEL=1 clears it)
     int32_t lean_wpl; // diagnostics: IRM_LEAN_WPL=2 forces two waypoints per lane at N ≤ 128
-    int32_t stagger, stagger_cyc;  // diagnostics (IRM_STAGGER): delay half the workgroups' loop start
-    int32_t lean2;  // the GD single loop of the N = 128, D = 3 shape on k_lean2 (two lanes per waypoint)
     float llr, lci, lsg0, ljl0, eps_p, eps_v, lmax, lreg;
     float bls_lr0, bls_a, bls_bp, bls_bm, vmax, pmax, pmin, pad1;
     // derived fp32 constants (reference casts its Python doubles to fp32)

@@ -593,7 +593,10 @@ __device__ void stage_alpha(const KParams& P, int tb0, int ntb, float* X, int xr
 //   q = fp32(fp32(K·α)[n]·J), v = fp32(fp32(dK·α)[n]·J).
 // (rs, cs: row / column strides of Xa — [row][16] LDS buffers by default, the lean kernel's
 // column-major buffers with rs = 1, cs = column stride)
-template <int D>
+// U: K / dK rows per software-pipelined batch (8 in the prologue / epilogue; the optimiser loop's resync
+// rounds use 2, which keeps the register peak of the dual-loop / BLS instantiations low — spill-free —
+// at the cost of less latency hiding in a round that runs once per outer iteration)
+template <int D, int U = 8>
 __device__ void eval_exact(const KParams& P, const float* __restrict__ Xa, int n, float (&q)[D], float (&v)[D],
                            const float* Kt = nullptr, const float* dKt = nullptr, int rs = kLd, int cs = 1) {
     const int N = P.N;
@@ -602,10 +605,9 @@ __device__ void eval_exact(const KParams& P, const float* __restrict__ Xa, int n
     for (int d = 0; d < D; ++d) aq[d] = av[d] = 0.0;
     const float* kt = (Kt ? Kt : P.Kt) + n;
     const float* dkt = (dKt ? dKt : P.dKt) + n;
-    // K / dK rows come from L2 / HBM: software-pipelined batches of 8 rows (the next batch's 16
+    // K / dK rows come from L2 / HBM: software-pipelined batches of U rows (the next batch's 2U
     // loads are in flight while this one is summed; the sum stays in the sequential order
     // m = 0, 1, …, N−1 of the oracle)
-    constexpr int U = 8;
     const int nb = N / U;
     int m0 = nb * U;
     if (nb > 0) {
@@ -2388,13 +2390,6 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // the older one in every phase; static priority for that half (MI355X_MICROARCH.md, two waves per
     // SIMD, item 4): C3 +1.7 %.  Priority only reorders issue: results are unchanged.
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-    if (P.stagger) {  // diagnostics: start half the workgroups' rounds late (phase offset between co-resident ones)
-        const bool late = P.stagger == 1 ? (blockIdx.x & 1) != 0 : blockIdx.x >= (gridDim.x + 1) / 2;
-        if (late) {
-            const long long t0 = clock64();
-            while (clock64() - t0 < P.stagger_cyc) __builtin_amdgcn_s_sleep(2);
-        }
-    }
     for (int par = 0;; par ^= 1) {
         f32x4 pre1[KQU1], pre1w[KQU1];
         if constexpr (kPre1) stage1_load(pre1, pre1w);
@@ -2494,7 +2489,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
                 for (int j = 0; j < WPL; ++j) {
                     if (vl[j]) {
-                        eval_exact<D>(P, X + (t * D) * ldx, nn[j], q[j], v[j], nullptr, nullptr, 1, ldx);
+                        eval_exact<D, 2>(P, X + (t * D) * ldx, nn[j], q[j], v[j], nullptr, nullptr, 1, ldx);
                         // the last extended-vis frame shows the exact trajectory of the returned α
                         if (rec && st.series_len > 0) {
 #pragma unroll
@@ -2793,8 +2788,6 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     if (tid == 0) prof.flush(P.prof);
 }
 
-#include "irm_lean2.hpp"
-
 // --------------------------------------------------- α-space eval kernels
 // mode 0: evaluate (K or dK)·α·J; 1: cost; 2: cost + grad; 3: constraints.
 // trajectory.py:63-65, 271-297, 129-180; same lane mapping as k_optimize.
@@ -3011,27 +3004,6 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s, LaunchDesc* de
                 q.NW = p.NW / 2;
                 if (p.lean_wpl == 2 && flow == LF_GD1 && lean_fits(q))
                     return launch_lean_one<Sh, 256, 2, false, LF_GD1>(q, grid, s, desc);
-            }
-        }
-        if constexpr (!Sh::kVariants && Sh::kNW == 128 && Sh::D == 3) {
-            // k_lean2: the GD single loop with two lanes per waypoint, 16 waves for up to 4 trajectories
-            if (p.lean2 && flow == LF_GD1 && p.TB <= 4) {
-                KParams q = p;
-                q.BT = 1024;
-                q.NW = 256;
-                if (lean2_lds(q) <= 160 * 1024) {
-                    if (desc) {
-                        char sn[48];
-                        shape_name<Sh>(sn, sizeof(sn));
-                        snprintf(desc->kernel, sizeof(desc->kernel), "k_lean2<%s,1024,LPW2,GD1>", sn);
-                        desc->lean = 1;
-                        desc->flow = LF_GD1;
-                        desc->wpl = 1;
-                        desc->rank_z = desc->rank_dir = 16;
-                        desc->rank_g = 24;
-                    }
-                    return run_optimizer(desc, k_lean2<Sh>, grid, 1024, lean2_lds(q), s, q);
-                }
             }
         }
         if constexpr (!Sh::kVariants && TT <= 512) {  // the lean kernel (F operators register-resident:

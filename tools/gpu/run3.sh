@@ -1,6 +1,6 @@
 cd $GRAFT_REPO_ROOT
 export PYTHONUNBUFFERED=1
-bash tools/gpu/stagger.sh || exit $?
+
 timeout -k 10 900 python -u -m pytest -v --timeout 300 --timeout-method thread tests/test_gpu_parity.py -k "ensemble or tracks_general or rank_cuts or launch_plan or batched" -s > gpurun_out/run3_tests.log 2>&1
 rc=$?; tail -4 gpurun_out/run3_tests.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "tests ended with $rc: stopping"; exit $rc; fi
