@@ -840,13 +840,22 @@ constexpr int shape_mp() {
 // One round of a workgroup (TB trajectories, one lane per waypoint):
 //   stage 1   y' = Fᵀ·[a'; b']          (MFMA, split-K over the waves → Ypart)
 //             a' = a·JᵀJ, b' = b·JᵀJ were mixed per lane when written, so y' = y·JᵀJ
-//   stage 2   Δ[T; V] = F·y'            (MFMA; B operand = Σ partials, summed on load)
-//   update    [T; V]' = c·[T; V] − s·Δ  (Δ latched in registers per direction)
+//   stage 2   G = (V_R·y')·J⁻¹ (MFMA tile set); GD also Δ[T; V] = F·y' (B operand = Σ partials,
+//             summed on load)
+//   update    GD:  [T; V]' = c·[T; V] − s·Δ  (Δ latched in registers per direction)
+//             BLS: [T; V]' = eval_exact(α_j), the trial's fp32 iterate (below)
 //   evaluate  cost at the trial point; gradient inputs for the next direction
 //   decide    the reference's accept / reject / λ logic per trajectory
-// α is not carried: each lane accumulates the gradient inputs of the accepted
-// steps (acc = c·acc + s·[a'; b']), and α = cprod·α_base − V_R·Fᵀ·acc·J⁻¹ is
-// formed only when an inner loop ends (PH_RESYNC).
+//   GD accept α' = fl(fl(c·α) − fl(lr·G)) per lane in fp32 with the reference's rounding, the rounding
+//             residual folded into the next direction through z = V_Rᵀ·e' (k_lean's scheme)
+// BLS: every trial's α_j = fl(fl(c_j·α) − fl(lr_j·ĝ)), ĝ = G/‖G‖ (optimizer_BLS.py:139, 165) is formed
+// per lane and its trajectory evaluated exactly, as the reference evaluates it: at N ≳ 500 (|α| ≈ 1e3,
+// singular K) one ulp of α moves the endpoint velocities by ~2e-3, so a trajectory that takes a trial's
+// rounding one step late (the GD scheme) decides a noise-dominated line search on other losses than the
+// reference (tools/e2e_ensemble.py: 47-67 gradient evaluations against the reference's 89-122 at
+// N = 500); the exact evaluation costs 2·N²·D fp64 FMAs per trial, this path's shapes are the small
+// batches outside k_lean's set.  Accepting a trial takes α_j and its [T; V] as they are.
+// When an inner loop ends (PH_RESYNC) [T; V] is replaced by eval_exact(α).
 // FULL (shape-specialised REGOPS launches of exactly MAXT threads): the stage-2 tiles per wave are
 // known exactly, so only those operator fragments occupy VGPRs (as in k_gd_single<…, FULL>).
 template <class S, int MAXT, bool OPS_LDS, bool REGOPS, bool BLS, bool FULL = false>
@@ -948,12 +957,12 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
     const float fb1 = yrow ? P.Fbot[(size_t)(N - 1) * RP + n] : 0.f;
     stage_obstacles(P, tb0, ntb, obsL);
     for (int e = tid; e < RP * kLd; e += P.BT) Ymix[e] = 0.f;
-    // GD: the rounding residual rows e' live in dP's direction columns between an accepted step and
-    // the next stage 1 (stage 2 rewrites dP only after the stage-1 barrier); none pending at start
+    // GD: the rounding residual rows e' live in dP's direction columns between an accepted step and the
+    // next stage 1 (stage 2 rewrites dP only after the stage-1 barrier); none pending at start
     if constexpr (!BLS)
         for (int e = tid; e < MP * kLd; e += P.BT) dP[e] = 0.f;
-    // GD: G's endpoint velocity columns for this lane's row (G = V_R·y'·J⁻¹, see the latch)
-    const float hv0 = (!BLS && valid) ? P.HV[n] : 0.f, hv1 = (!BLS && valid) ? P.HV[NK + n] : 0.f;
+    // G's endpoint velocity columns for this lane's row (G = V_R·y'·J⁻¹, see the latch)
+    const float hv0 = valid ? P.HV[n] : 0.f, hv1 = valid ? P.HV[NK + n] : 0.f;
     if (tid < 8) flagw[tid] = 0u;
     // Parameters used only on rare paths (outer-loop step, line search, resync, series) live in
     // LDS so that they hold no SGPRs across the loop.
@@ -996,11 +1005,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
     // T0 = (K·α0)·J, V0 = (dK·α0)·J  (trajectory.py:63-65), correctly rounded.
     // ab: this lane's row of the α the state is expressed against (α0, then the α
     // materialised at the last resync).
-    float q[D], v[D], s[D], g[D], ab[D], dT[D], dV[D], dra[D], drb[D], aca[D], acb[D], Gl[D];
+    float q[D], v[D], s[D], g[D], ab[D], dT[D], dV[D], Gl[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) {
         q[k] = v[k] = 0.f;
-        dT[k] = dV[k] = dra[k] = drb[k] = aca[k] = acb[k] = Gl[k] = 0.f;
+        dT[k] = dV[k] = Gl[k] = 0.f;
         ab[k] = valid ? X[n * kLd + t * D + k] : 0.f;
         s[k] = tvalid ? P.start[b * D + k] : 0.f;
         g[k] = tvalid ? P.goal[b * D + k] : 0.f;
@@ -1099,7 +1108,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
     };
 
     // replicated per-trajectory scalar state
-    float loss = 0.f, lsg = P.lsg0, ljl = P.ljl0, lr = 0.f, cprod = 1.f, gnorm = 1.f, anorm = 0.f;
+    float loss = 0.f, lsg = P.lsg0, ljl = P.ljl0, lr = 0.f, gnorm = 1.f, anorm = 0.f;
     float cfac = 1.f, step = 0.f;
     int phase = tvalid ? PH_OUTER_START : PH_DONE, outer = 0, inner = 0, trial = 0;
     bool needs_dir = false;
@@ -1123,20 +1132,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
         }
         // ------------------------------------------------ direction (stage 1+2)
         if (dirmask) {
-            // the direction's gradient inputs: this lane's rows (α recovery) and the two
-            // endpoint velocity rows of its trajectory (sparse stage 1)
-            // issued unconditionally (no branch, so the waits move to the first use after the
-            // stage-1 barrier); rows of invalid lanes are clamped and their values discarded
-            float e0[D], e1[D], xa[D], xb[D];
-            {
-                const int nr = valid ? n : 0;
+            // the two endpoint velocity rows of the trajectory's gradient inputs (sparse stage 1), read
+            // before stage 1 (the waits move to the first use after the stage-1 barrier)
+            float e0[D], e1[D];
 #pragma unroll
-                for (int k = 0; k < D; ++k) {
-                    xa[k] = X[nr * kLd + t * D + k];
-                    xb[k] = X[(NK + nr) * kLd + t * D + k];
-                    e0[k] = X[NK * kLd + t * D + k];
-                    e1[k] = X[(NK + N - 1) * kLd + t * D + k];
-                }
+            for (int k = 0; k < D; ++k) {
+                e0[k] = X[NK * kLd + t * D + k];
+                e1[k] = X[(NK + N - 1) * kLd + t * D + k];
             }
             IRM_STAMP(1);
             IRM_COUNT(13, dense);
@@ -1193,11 +1195,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                 }
             }
             IRM_STAMP(2);
-            // stage 2: dP = F(MP × RP)·Σ_s Ypart[s], only the direction columns
+            // stage 2: G tiles; GD also dP = F(MP × RP)·Σ_s Ypart[s], only the direction columns
             {
                 const float* xl = Ypart + (lane >> 4) * kLd + (lane & 15);
                 // y' rows (+ GD: z, the folded rounding residual, for the F tiles)
-                auto bload = [&](int i, float& b0, float& b1, float& b2, float& b3, bool withz = !BLS) {
+                auto bload = [&](int i, float& b0, float& b1, float& b2, float& b3, bool withz = true) {
                     b0 = b1 = b2 = b3 = 0.f;
                     for (int sp = 0; sp < nsplit; ++sp) {
                         const float* xb = xl + (sp * RP + i * 16) * kLd;
@@ -1214,9 +1216,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                         b3 += zb[12 * kLd];
                     }
                 };
-                if constexpr (!BLS) {
+                {
                     // G tiles: (V_R·y')[waypoint] into X's position rows (X was consumed by stage 1;
-                    // only the direction columns are written), from the top wave down
+                    // only the direction columns are written; every evaluation round rewrites X), from the
+                    // top wave down
                     for (int u = nwaves - 1 - wave; u < KQa; u += nwaves) {
                         const f32x4* ap = reinterpret_cast<const f32x4*>(P.VNs) + (size_t)u * KQ2 * 64 + lane;
                         f32x4 c0 = {0.f, 0.f, 0.f, 0.f};
@@ -1232,7 +1235,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                         store_tile(X, u, c0, dirmask);
                     }
                 }
-                if (REGOPS) {
+                if constexpr (BLS) {
+                    // BLS: no F tiles (the trial trajectories are evaluated exactly)
+                } else if (REGOPS) {
                     f32x4 acc[S2T];
 #pragma unroll
                     for (int j = 0; j < S2T; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1278,20 +1283,34 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
             __syncthreads();
             IRM_STAMP(3);
             if (needs_dir) {
-                // latch this lane's direction rows (+ the endpoint-velocity columns)
+                // GD: latch this lane's direction rows (+ the endpoint-velocity columns)
+                if constexpr (!BLS) {
 #pragma unroll
-                for (int k = 0; k < D; ++k) {
-                    dra[k] = valid ? xa[k] : 0.f;
-                    drb[k] = valid ? xb[k] : 0.f;
-                    float ut = dP[n * kLd + t * D + k], uv = dP[(NK + n) * kLd + t * D + k];
-                    // endpoint velocity rows: their operator columns in every round (stage 1's
-                    // operator has zero columns there)
-                    ut = fmaf(h0T, e0[k], fmaf(h1T, e1[k], ut));
-                    uv = fmaf(h0V, e0[k], fmaf(h1V, e1[k], uv));
-                    dT[k] = ut;
-                    dV[k] = uv;
+                    for (int k = 0; k < D; ++k) {
+                        float ut = dP[n * kLd + t * D + k], uv = dP[(NK + n) * kLd + t * D + k];
+                        // endpoint velocity rows: their operator columns in every round (stage 1's
+                        // operator has zero columns there)
+                        ut = fmaf(h0T, e0[k], fmaf(h1T, e1[k], ut));
+                        uv = fmaf(h0V, e0[k], fmaf(h1V, e1[k], uv));
+                        dT[k] = ut;
+                        dV[k] = uv;
+                    }
                 }
                 IRM_STAMP(16);
+                // G = (V_R·y')·J⁻¹ + its endpoint velocity columns (y' = y·JᵀJ, G = V_R·y·Jᵀ)
+                {
+                    float gr[D];
+#pragma unroll
+                    for (int k = 0; k < D; ++k)
+                        gr[k] = valid ? fmaf(hv0, e0[k], fmaf(hv1, e1[k], X[n * kLd + t * D + k])) : 0.f;
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        float gk = 0.f;
+#pragma unroll
+                        for (int l = 0; l < D; ++l) gk = fmaf(gr[l], cold[C_JINV + l * D + k], gk);
+                        Gl[k] = gk;
+                    }
+                }
                 if (bls) {
                     float tg = 0.f, ta = 0.f;
                     for (int ww = 0; ww < WPT; ++ww) {
@@ -1305,34 +1324,18 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                     phase = PH_BLS_TRIAL;
                     trial = 0;
                 } else {
-                    cfac = P.gd_c[outer];  // fp32(1 − λ_reg·lr) from the Python doubles (optimizer_GD.py:185)
+                    cfac = P.gd_c[outer];  // fp32(1 − λ_reg·lr) (optimizer_GD.py:185)
                     step = lr;
-                    // G = (V_R·y')·J⁻¹ + its endpoint velocity columns (y' = y·JᵀJ, G = V_R·y·Jᵀ)
-                    float gr[D];
-#pragma unroll
-                    for (int k = 0; k < D; ++k)
-                        gr[k] = valid ? fmaf(hv0, e0[k], fmaf(hv1, e1[k], X[n * kLd + t * D + k])) : 0.f;
-#pragma unroll
-                    for (int k = 0; k < D; ++k) {
-                        float gk = 0.f;
-#pragma unroll
-                        for (int l = 0; l < D; ++l) gk = fmaf(gr[l], cold[C_JINV + l * D + k], gk);
-                        Gl[k] = gk;
-                    }
                 }
                 needs_dir = false;
             }
         }
-        if (phase == PH_BLS_TRIAL) {
-            cfac = 1.f - P.lreg * lr;
-            step = lr / gnorm;
-        }
+        if (phase == PH_BLS_TRIAL) cfac = unfused(1.f - unfused(P.lreg * lr));  // (1 − λ_reg·bls_lr) in fp32 (optimizer_BLS.py:139)
         // ------------------------------------------------------- resync
-        // Trajectories whose inner loop ended last round: α = cprod·ab −
-        // V_R·(Fᵀ·acc)·J⁻¹ in fp32 (what the reference carries), then [T; V] =
-        // eval_exact(α), so the constraint check below and the caller's
-        // evaluate(α_out) see the same waypoints bit for bit.
-        if (rmask && !BLS) {  // block-uniform; GD: α is carried explicitly
+        // Trajectories whose inner loop ended last round: [T; V] = eval_exact(α) (α is the reference's
+        // fp32 iterate), so the constraint check below and the caller's evaluate(α_out) see the same
+        // waypoints bit for bit; GD's pending residual is absorbed.
+        if (rmask) {  // block-uniform; α is carried explicitly in fp32 (both optimisers)
             const bool rs = tvalid && ((rmask >> t) & 1u);  // wave-uniform
             if (rs && valid) {
 #pragma unroll
@@ -1352,68 +1355,32 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                 }
             }
         }
-        if (rmask && BLS) {  // block-uniform
-            const bool rs = tvalid && ((rmask >> t) & 1u);  // wave-uniform
-            if (rs && valid) {
-#pragma unroll
-                for (int k = 0; k < D; ++k) {
-                    X[n * kLd + t * D + k] = aca[k];
-                    X[(NK + n) * kLd + t * D + k] = acb[k];
-                }
-            }
-            __syncthreads();
-            stage1(true);
-            __syncthreads();
-            if (rs && yrow) {
-#pragma unroll
-                for (int d = 0; d < D; ++d) {
-                    // endpoint velocity rows through F's endpoint rows (stage 1's operator omits them)
-                    float y = fmaf(fb0, X[NK * kLd + t * D + d], fb1 * X[(NK + N - 1) * kLd + t * D + d]);
-                    for (int sp = 0; sp < nsplit; ++sp) y += Ypart[(sp * RP + n) * kLd + t * D + d];
-                    Ymix[n * kLd + t * D + d] = y;
-                }
-            }
-            __syncthreads();
-            if (rs && valid) {
-                float z[D];
-#pragma unroll
-                for (int l = 0; l < D; ++l) z[l] = 0.f;
-                const float* vr = cold_ptr(1) + (size_t)n * RP;
-                for (int r = 0; r < RP; ++r) {
-                    const float vv = vr[r];
-#pragma unroll
-                    for (int l = 0; l < D; ++l) z[l] += vv * Ymix[r * kLd + t * D + l];
-                }
-#pragma unroll
-                for (int k = 0; k < D; ++k) {
-                    float acc = 0.f;
-#pragma unroll
-                    for (int l = 0; l < D; ++l) acc += z[l] * cold[C_JINV + l * D + k];
-                    ab[k] = cprod * ab[k] - acc;
-                    X[n * kLd + t * D + k] = ab[k];
-                }
-            }
-            __syncthreads();
-            if (rs) {
-                if (valid) {
-                    eval_exact<D>(P, X + t * D, n, q, v, cold_ptr(2), cold_ptr(3));
-                    // the last extended-vis frame shows the materialised α's trajectory
-                    if (rec && st.series_len > 0) {
-                        float* ser = cold_ptr(0);
-                        const int ms = cold_int(C_MAXSER);
-#pragma unroll
-                        for (int k = 0; k < D; ++k) ser[((b * ms) + st.series_len - 1) * N * D + n * D + k] = q[k];
-                    }
-                }
-                cprod = 1.f;
-#pragma unroll
-                for (int k = 0; k < D; ++k) aca[k] = acb[k] = 0.f;
-            }
-        }
         IRM_STAMP(17);
         // ------------------------------------------------------- update
-        float q2[D], v2[D];
-        if (phase == PH_GD_INNER || phase == PH_BLS_TRIAL) {
+        float q2[D], v2[D], aj[BLS ? D : 1];
+        if constexpr (BLS) {
+            // the trial's α_j = fl(fl(c_j·α) − fl(lr_j·ĝ)), ĝ = G/‖G‖ (optimizer_BLS.py:139, 165), through
+            // X's position rows (consumed by this round's stage 1 and latch; rewritten by the gradient
+            // inputs after the evaluation barrier), [T; V] = eval_exact(α_j)
+            const bool trl = (phase == PH_BLS_TRIAL);  // wave-uniform
+            if (trl && valid) {
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    aj[k] = unfused(unfused(cfac * ab[k]) - unfused(lr * (Gl[k] / gnorm)));
+                    X[n * kLd + t * D + k] = aj[k];
+                }
+            }
+            __syncthreads();
+            if (trl && valid) {
+                eval_exact<D, 2>(P, X + t * D, n, q2, v2, cold_ptr(2), cold_ptr(3));
+            } else {
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    q2[k] = q[k];
+                    v2[k] = v[k];
+                }
+            }
+        } else if (phase == PH_GD_INNER) {
 #pragma unroll
             for (int k = 0; k < D; ++k) {
                 q2[k] = cfac * q[k] - step * dT[k];
@@ -1560,9 +1527,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                         inner++;
                         st.inner_iterations++;
                         snap = true;
-                        if (inner >= P.max_inner) to_end = true;
-                        else if (rejected_all) phase = PH_BLS_REEVAL;
-                        else needs_dir = true;
+                        if (inner >= P.max_inner) {
+                            to_end = true;
+                        } else if (rejected_all) {
+                            phase = PH_BLS_REEVAL;
+                        } else {
+                            needs_dir = true;
+                        }
                     }
                 }
             }
@@ -1596,14 +1567,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
             // --------------------------------------------------- accept
             if (accept == 1) {
                 if constexpr (BLS) {
+                    // the trial's α_j and its exactly evaluated [T; V]
 #pragma unroll
                     for (int k = 0; k < D; ++k) {
+                        ab[k] = aj[k];
                         q[k] = q2[k];
                         v[k] = v2[k];
-                        aca[k] = cfac * aca[k] + step * dra[k];  // α recovery: Σ steps·[a'; b']
-                        acb[k] = cfac * acb[k] + step * drb[k];
                     }
-                    cprod *= cfac;
                 } else {
                     // α' = fl(fl(c·α) − fl(lr·G)) (optimizer_GD.py:81, 185) and its residual e' = −e·J/lr
                     // for the next stage 1 (dP rows of this lane: stage 2 has been read)
@@ -1650,8 +1620,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
     }
 
     // ----------------------------------------------------------- epilogue
-    // Every trajectory ended through PH_RESYNC: acc = 0, cprod = 1, α = ab and
-    // T = eval_exact(α) exactly.
+    // Every trajectory ended through PH_RESYNC: α = ab and T = eval_exact(α) exactly.
     if (valid) {
 #pragma unroll
         for (int k = 0; k < D; ++k) {

@@ -996,3 +996,33 @@ def test_batched_bls_end_state_inside_oracle_ensemble():
         flip = first_decision_flip(tr, tro, float(args.loop_loss_reduction))
         print(f"  outside the ensemble's band: first decision flip {flip}")
         assert flip is not None and flip[1] <= BLS_KNIFE_EDGE, (b, flip)
+
+
+@pytest.mark.parametrize("case,argv,ov", [
+    ("n500", ["--n-timesteps", "500"], {}),
+    ("n100", ["--n-timesteps", "100"], {}),
+    ("whole_robot", [], {"whole_robot_cost": 1}),
+])
+def test_general_kernel_bls_follows_oracle_trial_for_trial(case, argv, ov):
+    """k_optimize's BLS (the shapes outside k_lean's set: N > 256, odd N, the whole-robot cost) carries α
+    in fp32 with the reference's rounding — α' = fl(fl(c_j·α) − fl(lr_j·G/‖G‖)) per accepted trial
+    (optimizer_BLS.py:139) — like k_lean.  From the same α0, its line-search log (problem 0) follows the
+    oracle's over 4 inner iterations trial for trial: accept / reject identical, lr exact, losses rtol
+    1e-3, ‖g‖ 2e-3 (the evaluation-point lag of test_batched_bls_line_search_follows_oracle)."""
+    from conftest import oracle_for
+    args = argv + ["--max-inner-iteration", "6", "--max-outer-iteration", "1", "--loop-loss-reduction=-1e30"]
+    c = ctx(*args, **ov)
+    assert c.launch_plan(1, 11)["lean"] == 0, c.launch_plan(1, 11)
+    c.bls_trace_enable(256)
+    a0 = c.init_alpha(START, GOAL)
+    _, _, st = c.optimize(START, GOAL, obstacles(), alpha0=a0)
+    tr = c.bls_trace(int(st["bls_trials"]))
+    o = oracle_for(*args, **ov)
+    _, so, tro = o.optimize_trace(a0, obstacles(), START, GOAL)
+    a, r = tr[tr[:, 1] < 4], tro[tro[:, 1] < 4]
+    print(f"{case}: {len(a)} trials in 4 inner iterations (oracle {len(r)}), accepted {a[:, 6].astype(int).tolist()}")
+    assert len(a) == len(r) and len(a) >= 4, (len(a), len(r))
+    np.testing.assert_array_equal(a[:, [0, 1, 2, 6]], r[:, [0, 1, 2, 6]])  # outer, inner, trial, accept
+    np.testing.assert_allclose(a[:, 3], r[:, 3], rtol=1e-7)  # lr
+    np.testing.assert_allclose(a[:, 4], r[:, 4], rtol=1e-3)  # new_loss
+    np.testing.assert_allclose(a[:, 8], r[:, 8], rtol=2e-3)  # |g|
