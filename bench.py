@@ -204,7 +204,7 @@ def pmc_traffic(cfg):
     for path in reversed(files):
         with open(path) as f:
             d = json.load(f)
-        if d.get("config", "c3") == cfg and d.get("hbm_bytes_per_launch"):
+        if d.get("config", "c3") == cfg and not d.get("faithful") and d.get("hbm_bytes_per_launch"):
             return float(d["hbm_bytes_per_launch"]), os.path.relpath(path, HERE)
     return None, None
 

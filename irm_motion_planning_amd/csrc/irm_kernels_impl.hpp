@@ -1744,7 +1744,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // stage-2 tiles per wave: all of this shape's tiles over the workgroup's waves (N = 256: 4)
     constexpr int S2X = (S::MP / 16 + MAXT / 64 - 1) / (MAXT / 64);
     constexpr int S2T = (FULL || S2X > kS2T(MAXT)) ? S2X : kS2T(MAXT);
-    constexpr bool RV = MAXT > 256 || WPL > 1;  // velocity half of stage 1 register-resident too
+    // velocity half of stage 1 register-resident too — except in the dual-loop / BLS flows beyond C3's
+    // shape, whose extra state leaves no room (read from L2 in the dense rounds there)
+    constexpr bool RV = (MAXT > 256 || WPL > 1) && (GD1 || (D == 3 && S::NK <= 128));
     constexpr int NWL = S::NW / WPL;  // lanes per trajectory
     constexpr int WPTL = NWL / 64;    // waves per trajectory
     constexpr bool VL = lean_vlds(S::NK, D, MAXT);  // V_R fragments staged in LDS (else read from L2)
@@ -1904,10 +1906,15 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     const float* obs = obsL + (P.obs_stride ? t * obs_pitch(P.O) : 0);
     // 9-12 obstacles (the reference's 11): the padded table in VGPRs for the whole launch (24 floats),
     // so the per-round evaluation does not wait on its LDS reads
-    f32x4 oreg[6];
+#ifndef IRM_X_OREG_ALL
+    constexpr bool OREG = GD1;
+#else
+    constexpr bool OREG = true;
+#endif
+    f32x4 oreg[OREG ? 6 : 1];
     const bool obs_reg = ((P.O + 3) >> 2) == 3;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) oreg[i] = obs_reg ? reinterpret_cast<const f32x4*>(obs)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < (OREG ? 6 : 1); ++i) oreg[i] = obs_reg ? reinterpret_cast<const f32x4*>(obs)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
     // replicated per-trajectory state
     float lsg = P.lsg0, ljl = P.ljl0;
     float lr = BLS ? P.bls_lr0 : P.gd_lr[0];
@@ -1931,7 +1938,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         }
 #pragma unroll
         for (int j = 0; j < WPL; ++j) {
-            if (WPL == 1 && vl[j]) eval_waypoint<D>(P, q2[j], v2[j], obs, w[j], oreg);  // oreg: read only when nq == 3
+            if (WPL == 1 && vl[j]) eval_waypoint<D>(P, q2[j], v2[j], obs, w[j], OREG ? oreg : nullptr);  // oreg: read only when nq == 3
             cvs[j] = w[j].cv;
             const float u = P.one_m_lmax * (w[j].cv * P.invN) + ljl_e * ((w[j].jp + w[j].jv) * P.invN);
             if (j == 0) {
@@ -1955,7 +1962,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 float a = 0.f, bb = 0.f;
 #pragma unroll
                 for (int d = 0; d < D; ++d) {
-                    const float e = q2[j][d] - (n == 0 ? s[d] : g[d]);
+                    const float e = q2[j][d] - tg[j][d];  // tg: s on row 0, g on row N − 1
                     a += e * e;
                     bb += v2[j][d] * v2[j][d];
                 }

@@ -16,4 +16,4 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch"
     python3 "$ROOT/bench.py" --no-cpu-baseline --steps 5 --warmup 1 "$@" > "$OUT/fetch.log" 2>&1 || { echo "fetch pass failed"; exit 3; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
     python3 "$ROOT/bench.py" --no-cpu-baseline --steps 5 --warmup 1 "$@" > "$OUT/write.log" 2>&1 || { echo "write pass failed"; exit 3; }
-cd "$ROOT" && python3 tools/summarize_profile.py "$R" "$OUT"
+cd "$ROOT" && python3 tools/summarize_profile.py "$R" "$OUT" "$@"

@@ -34,12 +34,16 @@ def counter_rows(path, kernel_subs=("k_lean", "k_optimize")):
 
 def main():
     tag, out = sys.argv[1], sys.argv[2]
+    extra = sys.argv[3:]
+    cfg = extra[extra.index("--config") + 1] if "--config" in extra else "c3"
     prof = os.path.join(HERE, "profiles")
     os.makedirs(prof, exist_ok=True)
     stats = find(os.path.join(out, "stats"), "*kernel_stats.csv")
     if stats:
         shutil.copy(stats, os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    res = {"round": tag, "kernel": "irm::k_lean / irm::k_optimize (the optimiser launch)", "command": "python bench.py --no-cpu-baseline --steps 5 --warmup 1"}
+    res = {"round": tag, "config": cfg, "faithful": "--faithful" in extra,
+           "kernel": "irm::k_lean / irm::k_optimize (the optimiser launch)",
+           "command": "python bench.py --no-cpu-baseline --steps 5 --warmup 1 " + " ".join(extra)}
     for name, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
         path = find(os.path.join(out, sub), "*counter_collection.csv")
         if not path:

@@ -1,4 +1,4 @@
-"""Per-dispatch SQ counter means of k_optimize from tools/pmc_sq.sh output."""
+"""Per-dispatch SQ counter means of the optimiser launch (k_lean / k_optimize) from tools/pmc_sq.sh output."""
 import csv
 import glob
 import os
