@@ -128,6 +128,7 @@ typedef struct irm_info {
     int32_t lds_bytes_optimize; /* LDS per optimiser workgroup             */
     char device_name[64];
     char arch[32];
+    char build_id[24];          /* = irm_build_id(): source hash of the build */
 } irm_info;
 
 /* Device-pointer batch for irm_optimize_batch_dev.  All pointers are device

@@ -97,6 +97,7 @@ class IrmInfo(ctypes.Structure):
         ("lds_bytes_optimize", ctypes.c_int32),
         ("device_name", ctypes.c_char * 64),
         ("arch", ctypes.c_char * 32),
+        ("build_id", ctypes.c_char * 24),
     ]
 
 

@@ -11,8 +11,8 @@ class _PersistentOptimizer:
     """Reference object API: Optimizer(args); .optimize() -> α; .env; .trajectory.
 
     optimize() runs the whole outer/inner(/line-search) loop of the reference's
-    jit variant in one launch of k_optimize.  With --extended-vis it also
-    returns the per-iteration trajectory series the reference's plain loop
+    jit variant in one persistent launch (k_lean or k_optimize, Context.launch_plan).
+    With --extended-vis it also returns the per-iteration trajectory series the reference's plain loop
     records (in both loop modes — the reference supports it only with
     --jit-loop false).
     """

@@ -73,6 +73,7 @@ class Context:
         d = {name: getattr(inf, name) for name, _ in IrmInfo._fields_}
         d["device_name"] = d["device_name"].decode()
         d["arch"] = d["arch"].decode()
+        d["build_id"] = d["build_id"].decode()
         return d
 
     def launch_plan(self, batch, n_obstacles=0, series=False):

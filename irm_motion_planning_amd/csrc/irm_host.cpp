@@ -864,6 +864,7 @@ int irm_get_info(const irm_ctx* c, irm_info* out) {
     out->lds_bytes_optimize = c->lds_opt;
     snprintf(out->device_name, sizeof(out->device_name), "%s", c->name);
     snprintf(out->arch, sizeof(out->arch), "%s", c->arch);
+    snprintf(out->build_id, sizeof(out->build_id), "%s", irm_build_id());
     return IRM_OK;
 }
 

@@ -7,8 +7,9 @@ the CPU tests) are exactly the four §8e lists:
 1. broadcast of the shared environment (obstacles, and start/goal when rank 0
    owns them) from rank 0 — broadcast_environment;
 2. none inside the optimiser (K, dK, F are rebuilt deterministically per rank);
-3. all-gather of the per-rank α / trajectories / statistics so that rank 0 can
-   write the batch files — gather_batch (shards padded to the largest one);
+3. gather of the per-rank α / trajectories / statistics to rank 0, which writes
+   the batch files — gather_batch (shards padded to the largest one; the other
+   ranks receive nothing);
 4. the scalar reductions of the benchmark (max elapsed, Σ iterations) —
    reduce_timing.
 
@@ -54,9 +55,9 @@ def broadcast_environment(obstacles, start=None, goal=None, device="cpu", src=0)
     return tuple(out)
 
 
-def gather_batch(arrays, B, device="cpu"):
-    """All-gather per-rank shards (dict name -> array with leading dim = this rank's shard size)
-    into global arrays (leading dim B, rank order) on every rank."""
+def gather_batch(arrays, B, device="cpu", dst=0):
+    """Gather per-rank shards (dict name -> array with leading dim = this rank's shard size) to rank
+    `dst`: there, global arrays (leading dim B, rank order); None on every other rank."""
     import torch
     dist = _dist()
     world, rank = dist.get_world_size(), dist.get_rank()
@@ -71,10 +72,11 @@ def gather_batch(arrays, B, device="cpu"):
         buf = np.zeros((mx,) + a.shape[1:], dtype=dt)
         buf[: a.shape[0]] = a
         t = torch.from_numpy(buf).to(device)
-        parts = [torch.empty_like(t) for _ in range(world)]
-        dist.all_gather(parts, t)
-        out[name] = np.concatenate([p.cpu().numpy()[: sizes[r]] for r, p in enumerate(parts)], axis=0)
-    return out
+        parts = [torch.empty_like(t) for _ in range(world)] if rank == dst else None
+        dist.gather(t, parts, dst=dst)
+        if rank == dst:
+            out[name] = np.concatenate([p.cpu().numpy()[: sizes[r]] for r, p in enumerate(parts)], axis=0)
+    return out if rank == dst else None
 
 
 def reduce_timing(elapsed, iterations, device="cpu"):

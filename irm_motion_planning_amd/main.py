@@ -125,7 +125,7 @@ def run_batch(optimizer, args):
 
     Under torchrun (WORLD_SIZE > 1, one process per GPU) the batch is sharded:
     rank 0's environment and problems are broadcast, every rank optimises its rows
-    [lo, hi), the results are all-gathered and rank 0 reports and writes the files."""
+    [lo, hi), the results are gathered to rank 0, which reports and writes the files."""
     env, tr = optimizer.env, optimizer.trajectory
     world, rank, _ = distributed.world_info()
     B = args.batch_size
@@ -159,12 +159,12 @@ def run_batch(optimizer, args):
         parts.update({"stat_" + k: np.asarray(v) for k, v in stats.items()})
         if series is not None:
             parts["series"] = series
-        full = distributed.gather_batch(parts, B, dev)
+        full = distributed.gather_batch(parts, B, dev)  # rank 0 only
+        if rank != 0:
+            return alpha  # this rank's shard
         alpha, traj = full["alpha"], full["traj"]
         stats = {k[5:]: v for k, v in full.items() if k.startswith("stat_")}
         series = full.get("series")
-        if rank != 0:
-            return alpha
     avg = tr.compute_trajectory_cost(alpha, env.obstacles, start, goal, 0, 0, 0)
     mx = tr.compute_trajectory_cost(alpha, env.obstacles, start, goal, 0, 0, 1)
     ok, _ = optimizer.context.constraints(alpha, start, goal)

@@ -2,9 +2,10 @@
 
 Squared-penalty dual loop with normalised-gradient steps and Armijo
 backtracking (trial loop optimizer_BLS.py:131-150, inner loop 154-179, outer
-loop 183-211), all inside the persistent kernel k_optimize: the search
-direction is computed once per inner iteration and every trial step is a
-pure per-waypoint evaluation (no kernel-matrix products).
+loop 183-211), all inside one persistent launch (k_lean for the specialised
+shapes: the search direction is computed once per inner iteration and every
+trial step is a per-waypoint evaluation; k_optimize otherwise: each trial's
+fp32 iterate evaluated exactly).
 """
 from ._optimizer import _PersistentOptimizer
 

@@ -4,7 +4,8 @@ Fixed-step functional gradient descent.  With max_outer_iteration > 1 it is
 the dual loop (jit_dual_optimize, optimizer_GD.py:173-232: per-outer step
 size gd_lr[outer], λ escalation on violated constraints); with 1 it is the
 single loop (jit_optimize, optimizer_GD.py:68-97).  Both run on device in
-the persistent kernel k_optimize.
+one persistent launch: k_lean for the specialised shapes (the bench path),
+k_optimize otherwise (the library's launch plan names the kernel).
 """
 from ._abi import IrmError
 from ._optimizer import _PersistentOptimizer

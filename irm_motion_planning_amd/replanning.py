@@ -12,7 +12,7 @@ straight line of initTrajectory (optimizer_BLS.py:57-62).
   every call; only the new obstacles / start / goal are copied in;
 * with warm_start the next plan starts from the previous plan's α, which never
   leaves HBM (α_out of call k is α0 of call k+1, double-buffered);
-* each call is one launch of k_optimize through irm_optimize_batch_dev on the
+* each call is one optimiser launch (k_lean / k_optimize) through irm_optimize_batch_dev on the
   caller's stream (torch provides device memory and the stream).
 
 The first call, or warm_start=False, is exactly Optimizer.optimize() for the batch.

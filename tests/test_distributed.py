@@ -99,15 +99,16 @@ def _gather_worker(rank, world, port, out_dir):
     ok = (np.arange(lo, hi) % 2).astype(np.uint8)
     full = D.gather_batch({"traj": traj, "iters": iters, "ok": ok}, B)
     t_max, it_sum = D.reduce_timing(0.5 * (rank + 1), hi - lo)
+    assert (full is None) == (rank != 0)  # gathered to rank 0 only
     np.savez(os.path.join(out_dir, f"g{rank}.npz"), obs=obs, s=s, lo=lo, hi=hi, t_max=t_max, it_sum=it_sum,
-             **full)
+             **(full or {}))
     dist.barrier()
     dist.destroy_process_group()
 
 
 def test_distributed_helpers_two_ranks(tmp_path):
     """irm_motion_planning_amd.distributed over gloo, world 2: broadcast of rank 0's environment,
-    contiguous uneven shards, all-gather of float/int/uint8 per-problem results in rank order,
+    contiguous uneven shards, gather of float/int/uint8 per-problem results to rank 0 in rank order,
     max/sum timing reduction (the nccl path of main.py --batch-size under torchrun)."""
     world = 2
     mp.start_processes(_gather_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
@@ -120,11 +121,13 @@ def test_distributed_helpers_two_ranks(tmp_path):
     for x in r:
         np.testing.assert_array_equal(x["obs"], obs0)
         np.testing.assert_array_equal(x["s"], s0)
-        np.testing.assert_array_equal(x["traj"], np.repeat(s0[:, None, :], 5, axis=1) * np.float32(2))
-        np.testing.assert_array_equal(x["iters"], np.arange(7) * 10)
-        assert x["iters"].dtype == np.int64 and x["ok"].dtype == np.uint8
-        np.testing.assert_array_equal(x["ok"], np.arange(7) % 2)
         assert float(x["t_max"]) == 1.0 and float(x["it_sum"]) == 7
+    x = r[0]  # the gathered batch, on rank 0
+    np.testing.assert_array_equal(x["traj"], np.repeat(s0[:, None, :], 5, axis=1) * np.float32(2))
+    np.testing.assert_array_equal(x["iters"], np.arange(7) * 10)
+    assert x["iters"].dtype == np.int64 and x["ok"].dtype == np.uint8
+    np.testing.assert_array_equal(x["ok"], np.arange(7) % 2)
+    assert "traj" not in r[1]
 
 
 def test_shard_tiles_batch():

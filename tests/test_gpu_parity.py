@@ -405,6 +405,14 @@ def test_bench_c7_seven_dof_n128():
     _bench_vs_ref("c7", 64, 4)
 
 
+def test_context_info_carries_the_build_id():
+    """irm_get_info reports the source hash of the library that runs (the same as irm_build_id), so a
+    deployment can check it against the sources it ships."""
+    from irm_motion_planning_amd import build
+    inf = ctx().info()
+    assert inf["build_id"] == build.source_hash() and inf["abi_version"] == 3, inf
+
+
 @pytest.mark.parametrize("cfg,faithful,B,want", [
     ("c3", False, 1024, "k_lean<FixShape<3,128,32>,512,1,FULL,GD1>"),
     ("c3", True, 1024, "k_lean<FixShape<3,128,32>,512,1,FULL,GD2>"),
