@@ -1358,6 +1358,12 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
         IRM_STAMP(17);
         // ------------------------------------------------------- update
         float q2[D], v2[D], aj[BLS ? D : 1];
+        // (K / dK rows per pipelined batch of the trial's exact evaluation: 8, as the resync's)
+#ifndef IRM_X_TRIAL_U
+        constexpr int kTrialU = 8;
+#else
+        constexpr int kTrialU = IRM_X_TRIAL_U;
+#endif
         if constexpr (BLS) {
             // the trial's α_j = fl(fl(c_j·α) − fl(lr_j·ĝ)), ĝ = G/‖G‖ (optimizer_BLS.py:139, 165), through
             // X's position rows (consumed by this round's stage 1 and latch; rewritten by the gradient
@@ -1372,7 +1378,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
             }
             __syncthreads();
             if (trl && valid) {
-                eval_exact<D, 2>(P, X + t * D, n, q2, v2, cold_ptr(2), cold_ptr(3));
+                eval_exact<D, kTrialU>(P, X + t * D, n, q2, v2, cold_ptr(2), cold_ptr(3));
             } else {
 #pragma unroll
                 for (int k = 0; k < D; ++k) {
@@ -2350,6 +2356,15 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     __syncthreads();
 
     IRM_STAMP(14);
+    // K / dK rows per software-pipelined batch of the resync's eval_exact: the loads are latency-bound
+    // (one L2 round trip per batch), so D = 3 with one waypoint per lane takes 8 rows per batch — no extra
+    // spills there (C3 faithful 4.57 -> 4.42 ms, C3 BLS faithful 5.68 -> 5.60, C2 0.706 -> 0.689, same
+    // box, same sums in the same order); the D = 7 / two-waypoint variants keep 2 (register peak)
+#ifndef IRM_X_RESYNC_U
+    constexpr int kResyncU = (D <= 3 && WPL == 1) ? 8 : 2;
+#else
+    constexpr int kResyncU = (D <= 3 && WPL == 1) ? IRM_X_RESYNC_U : 2;
+#endif
     // ---------------------------------------------------------- rounds
     float dTl[BLS ? WPL : 1][D], dVl[BLS ? WPL : 1][D], Gl[BLS ? WPL : 1][D];  // BLS: latched direction
     // BLS: the rounding residual not yet in [T; V] (α units) and the reference step it is folded into
@@ -2465,7 +2480,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
                 for (int j = 0; j < WPL; ++j) {
                     if (vl[j]) {
-                        eval_exact<D, 2>(P, X + (t * D) * ldx, nn[j], q[j], v[j], nullptr, nullptr, 1, ldx);
+                        eval_exact<D, kResyncU>(P, X + (t * D) * ldx, nn[j], q[j], v[j], nullptr, nullptr, 1, ldx);
                         // the last extended-vis frame shows the exact trajectory of the returned α
                         if (rec && st.series_len > 0) {
 #pragma unroll
