@@ -603,8 +603,12 @@ __device__ void eval_exact(const KParams& P, const float* __restrict__ Xa, int n
     double aq[D], av[D];
 #pragma unroll
     for (int d = 0; d < D; ++d) aq[d] = av[d] = 0.0;
-    const float* kt = (Kt ? Kt : P.Kt) + n;
-    const float* dkt = (dKt ? dKt : P.dKt) + n;
+    // wave-uniform bases and 32-bit element offsets (global loads with an SGPR base and a VGPR
+    // offset): inside the optimiser loop a per-lane 64-bit pointer would be hoisted out of the loop
+    // and held (or spilled) across every round
+    const float* kt = Kt ? Kt : P.Kt;
+    const float* dkt = dKt ? dKt : P.dKt;
+    const unsigned un = (unsigned)n, uN = (unsigned)N;
     // K / dK rows come from L2 / HBM: software-pipelined batches of U rows (the next batch's 2U
     // loads are in flight while this one is summed; the sum stays in the sequential order
     // m = 0, 1, …, N−1 of the oracle)
@@ -614,8 +618,8 @@ __device__ void eval_exact(const KParams& P, const float* __restrict__ Xa, int n
         float kq[U], kv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            kq[u] = kt[(size_t)u * N];
-            kv[u] = dkt[(size_t)u * N];
+            kq[u] = kt[(unsigned)u * uN + un];
+            kv[u] = dkt[(unsigned)u * uN + un];
         }
         for (int bi = 0; bi < nb; ++bi) {
             const int mb = bi * U;
@@ -623,8 +627,8 @@ __device__ void eval_exact(const KParams& P, const float* __restrict__ Xa, int n
             const int mn = (bi + 1 < nb) ? mb + U : mb;  // (the last batch re-reads itself: no branch)
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                nq[u] = kt[(size_t)(mn + u) * N];   // K[n][m]
-                nv[u] = dkt[(size_t)(mn + u) * N];  // dK[n][m]
+                nq[u] = kt[(unsigned)(mn + u) * uN + un];   // K[n][m]
+                nv[u] = dkt[(unsigned)(mn + u) * uN + un];  // dK[n][m]
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -644,7 +648,7 @@ __device__ void eval_exact(const KParams& P, const float* __restrict__ Xa, int n
         }
     }
     for (int m = m0; m < N; ++m) {
-        const double kq = (double)kt[(size_t)m * N], kv = (double)dkt[(size_t)m * N];
+        const double kq = (double)kt[(unsigned)m * uN + un], kv = (double)dkt[(unsigned)m * uN + un];
         const float* xr = Xa + m * rs;
 #pragma unroll
         for (int d = 0; d < D; ++d) {

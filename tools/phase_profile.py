@@ -43,7 +43,8 @@ def run(cfg, tb=0, rank=0, faithful=False):
     buf = (ctypes.c_uint64 * (nb * K))()
     n = ctx.lib.irm_debug_phase_profile(ctx.handle, buf, nb)
     prof = np.frombuffer(buf, dtype=np.uint64, count=n * K).reshape(n, K).astype(np.float64)
-    rounds = float(np.max(st["grad_evals"]) + np.max(st["outer_iterations"]))
+    per = st["bls_trials"] if args.optimizer_name == "bls" else st["grad_evals"]  # one round per trial / step
+    rounds = float(np.max(per) + np.max(st["outer_iterations"]))
     tot = prof.sum(1) - prof[:, 13]
     print(f"== {cfg} tb={info['traj_per_block']} R={info['operator_rank']} blocks={n} host {1000*dt:.2f} ms "
           f"rounds~{rounds:.0f} total cycles/block mean {tot.mean():.0f} -> {tot.mean()/rounds:.0f} per round")
