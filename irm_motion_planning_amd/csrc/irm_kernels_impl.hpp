@@ -180,11 +180,13 @@ __device__ __forceinline__ void sincos_poly(float x, float& sn, float& cs) {
     const float sp = fmaf(r * z, fmaf(z, fmaf(z, -1.9515295891e-4f, 8.3321608736e-3f), -1.6666654611e-1f), r);
     const float cp = fmaf(z * z, fmaf(z, fmaf(z, 2.443315711809948e-5f, -1.388731625493765e-3f), 4.166664568298827e-2f),
                           fmaf(-0.5f, z, 1.0f));
-    const int q = (int)kf & 3;
-    const float s0 = (q & 1) ? cp : sp;
-    const float c0 = (q & 1) ? sp : cp;
-    sn = (q & 2) ? -s0 : s0;
-    cs = ((q + 1) & 2) ? -c0 : c0;
+    // quadrant q = kf mod 4: swap on odd q, sin negated for q ∈ {2, 3}, cos for q ∈ {1, 2} — the sign
+    // flips as bit 1 of q (resp. q + 1) moved to the sign bit (an xor; −x and the flip agree bit for bit)
+    const int qi = (int)kf;
+    const float s0 = (qi & 1) ? cp : sp;
+    const float c0 = (qi & 1) ? sp : cp;
+    sn = __uint_as_float(__float_as_uint(s0) ^ (((unsigned)qi << 30) & 0x80000000u));
+    cs = __uint_as_float(__float_as_uint(c0) ^ (((unsigned)(qi + 1) << 30) & 0x80000000u));
 }
 __device__ __forceinline__ void sincos_fast(float x, float& sn, float& cs) {
     if (__builtin_expect(fabsf(x) > 1.0e4f, 0)) {
@@ -1985,24 +1987,69 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         float nl, tx, tn, va, a0, b0, a1, b1;
         int idx;
     };
+    // Latency-hiding load batches (finalize's records and start/goal terms, stage 2's split-K partial
+    // sums, the z unit's operands) hold more values live at once: used for the D = 3, N <= 128 shapes,
+    // where they fit without spills; at N = 256 or D = 7 they pushed the spill-free GD single-loop
+    // variants into scratch (C5: 14 spilled VGPRs)
+    constexpr bool kLat = D <= 3 && S::kNW > 0 && S::NK <= 128;
     auto finalize = [&](float lsg_e) {
-        const float* r0 = red + (t * WPTL) * 8;
-        float cmax = r0[0];
-        int cidx = __float_as_int(r0[1]);
-        float usum = r0[2], tx = r0[3], tn = r0[4], va = r0[5];
+        if constexpr (!kLat) {
+            const float* r0 = red + (t * WPTL) * 8;
+            float cmax = r0[0];
+            int cidx = __float_as_int(r0[1]);
+            float usum = r0[2], tx = r0[3], tn = r0[4], va = r0[5];
+            for (int ww = 1; ww < WPTL; ++ww) {
+                const float* rw = red + (t * WPTL + ww) * 8;
+                amax_step(cmax, cidx, rw[0], __float_as_int(rw[1]));
+                usum += rw[2];
+                tx = fmaxf(tx, rw[3]);
+                tn = fminf(tn, rw[4]);
+                va = fmaxf(va, rw[5]);
+            }
+            Fin f;
+            f.a0 = sg[t * 4 + 0];
+            f.b0 = sg[t * 4 + 1];
+            f.a1 = sg[t * 4 + 2];
+            f.b1 = sg[t * 4 + 3];
+            const float sgpc = 0.5f * f.a0 + 0.5f * f.a1;  // trajectory.py:187
+            const float sgvc = 0.5f * f.b0 + 0.5f * f.b1;  // trajectory.py:203
+            f.nl = (P.lam_max * cmax + usum) + lsg_e * (sgpc + sgvc);
+            f.idx = cidx;
+            f.tx = tx;
+            f.tn = tn;
+            f.va = va;
+            return f;
+        }
+        // every wave record and the start/goal terms are read before the first use (one LDS round trip;
+        // the argmax merge as selects, so no read is sunk into a branch)
+        float rr[WPTL][6], sgr[4];
+#pragma unroll
+        for (int ww = 0; ww < WPTL; ++ww)
+#pragma unroll
+            for (int e = 0; e < 6; ++e) rr[ww][e] = red[(t * WPTL + ww) * 8 + e];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sgr[e] = sg[t * 4 + e];
+        __builtin_amdgcn_sched_barrier(0);
+        float cmax = rr[0][0];
+        int cidx = __float_as_int(rr[0][1]);
+        float usum = rr[0][2], tx = rr[0][3], tn = rr[0][4], va = rr[0][5];
+#pragma unroll
         for (int ww = 1; ww < WPTL; ++ww) {
-            const float* rw = red + (t * WPTL + ww) * 8;
-            amax_step(cmax, cidx, rw[0], __float_as_int(rw[1]));
-            usum += rw[2];
-            tx = fmaxf(tx, rw[3]);
-            tn = fminf(tn, rw[4]);
-            va = fmaxf(va, rw[5]);
+            const float ov = rr[ww][0];
+            const int oi = __float_as_int(rr[ww][1]);
+            const bool take = ov > cmax || (ov == cmax && oi < cidx);  // amax_step
+            cmax = take ? ov : cmax;
+            cidx = take ? oi : cidx;
+            usum += rr[ww][2];
+            tx = fmaxf(tx, rr[ww][3]);
+            tn = fminf(tn, rr[ww][4]);
+            va = fmaxf(va, rr[ww][5]);
         }
         Fin f;
-        f.a0 = sg[t * 4 + 0];
-        f.b0 = sg[t * 4 + 1];
-        f.a1 = sg[t * 4 + 2];
-        f.b1 = sg[t * 4 + 3];
+        f.a0 = sgr[0];
+        f.b0 = sgr[1];
+        f.a1 = sgr[2];
+        f.b1 = sgr[3];
         const float sgpc = 0.5f * f.a0 + 0.5f * f.a1;  // trajectory.py:187
         const float sgvc = 0.5f * f.b0 + 0.5f * f.b1;  // trajectory.py:203
         f.nl = (P.lam_max * cmax + usum) + lsg_e * (sgpc + sgvc);
@@ -2137,6 +2184,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 a[i] = ap[(size_t)i * 64];
                 bb[i] = *reinterpret_cast<const f32x4*>(el + (sp * KQZ + i) * 16);
             }
+            if constexpr (kLat) __builtin_amdgcn_sched_barrier(0);  // all loads in flight before the first MFMA
             f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int i = 0; i < KQZ; ++i) {
@@ -2175,6 +2223,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // accumulation order per tile as the general form below)
     constexpr int kMTG = S::NK / 16, kGT = (kMTG + MAXT / 64 - 1) / (MAXT / 64);
     constexpr bool kS2Fix = FULL && S::kNW > 0;
+    constexpr bool kS2Batch = kS2Fix && kLat;  // stage 2's partial sums read in one batch
     auto stage2 = [&]() {
         f32x4 acc[S2T];
 #pragma unroll
@@ -2188,13 +2237,43 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 ga[g][0] = ga[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
                 if (u < kMTG) {
                     ga[g][0] = ap[0];
-                    ga[g][1] = ap[64];
+                    const f32x2 h = *reinterpret_cast<const f32x2*>(ap + 64);  // kR24: MFMAs 0-1 only
+                    ga[g][1] = f32x4{h.x, h.y, 0.f, 0.f};
                 }
             }
         }
         f32x4 by[2], bt[2];
+        if constexpr (kS2Batch) {
+            // every split-K partial of y'' and z is read before the first sum (one LDS round trip; the
+            // machine scheduler otherwise reuses one register quad for the reads and waits after each,
+            // seven round trips per round); same sums in the same order as the general form below
+            // (the second k-quad feeds only the G tiles' MFMAs 0-1 (kR24): its rows 0-1 of each quad)
+            constexpr int NS = S::NSPLIT;
+            f32x4 yp[NS], zq[kZS];
+            f32x2 yq[NS];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+            for (int sp = 0; sp < NS; ++sp) {
+                yp[sp] = *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + cl) * ldy + r4x);
+                yq[sp] = *reinterpret_cast<const f32x2*>(Ypart + (sp * 16 + cl) * ldy + 16 + r4x);
+            }
+#pragma unroll
+            for (int sp = 0; sp < kZS; ++sp) zq[sp] = *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + r4x);
+            __builtin_amdgcn_sched_barrier(0);
+            f32x4 bz = {0.f, 0.f, 0.f, 0.f};
+            f32x2 b1 = {0.f, 0.f};
+            by[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int sp = 0; sp < NS; ++sp) {
+                by[0] += yp[sp];
+                b1 += yq[sp];
+            }
+#pragma unroll
+            for (int sp = 0; sp < kZS; ++sp) bz += zq[sp];
+            bt[0] = by[0] + bz;
+            by[1] = bt[1] = f32x4{b1.x, b1.y, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int i = 0; i < (kS2Batch ? 0 : 2); ++i) {
             by[i] = bt[i] = f32x4{0.f, 0.f, 0.f, 0.f};
             if (i < KQ2) {
                 f32x4 bz = {0.f, 0.f, 0.f, 0.f};
