@@ -2237,8 +2237,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 ga[g][0] = ga[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
                 if (u < kMTG) {
                     ga[g][0] = ap[0];
-                    const f32x2 h = *reinterpret_cast<const f32x2*>(ap + 64);  // kR24: MFMAs 0-1 only
-                    ga[g][1] = f32x4{h.x, h.y, 0.f, 0.f};
+                    ga[g][1] = ap[64];
                 }
             }
         }
@@ -2248,16 +2247,22 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             // machine scheduler otherwise reuses one register quad for the reads and waits after each,
             // seven round trips per round); same sums in the same order as the general form below
             // (the second k-quad feeds only the G tiles' MFMAs 0-1 (kR24): its rows 0-1 of each quad)
+            // (read as whole quads: the swizzled layout is conflict-free for ds_read_b128, not for the
+            // b64 reads the compiler narrows these to — SQ_LDS_BANK_CONFLICT 0.8 M -> 4.1 M cycles)
             constexpr int NS = S::NSPLIT;
-            f32x4 yp[NS], zq[kZS];
-            f32x2 yq[NS];
+            f32x4 yp[NS], zq[kZS], yq[NS];
 #pragma unroll
             for (int sp = 0; sp < NS; ++sp) {
                 yp[sp] = *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + cl) * ldy + r4x);
-                yq[sp] = *reinterpret_cast<const f32x2*>(Ypart + (sp * 16 + cl) * ldy + 16 + r4x);
+                yq[sp] = *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + cl) * ldy + 16 + r4x);
             }
 #pragma unroll
             for (int sp = 0; sp < kZS; ++sp) zq[sp] = *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + r4x);
+            // every quad stays whole (no narrowing, no register reuse of its unused half while in flight)
+#pragma unroll
+            for (int sp = 0; sp < NS; ++sp) asm volatile("" ::"v"(yq[sp]));
+#pragma unroll
+            for (int g = 0; g < kGT; ++g) asm volatile("" ::"v"(ga[g][1]));
             __builtin_amdgcn_sched_barrier(0);
             f32x4 bz = {0.f, 0.f, 0.f, 0.f};
             f32x2 b1 = {0.f, 0.f};
@@ -2265,7 +2270,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
             for (int sp = 0; sp < NS; ++sp) {
                 by[0] += yp[sp];
-                b1 += yq[sp];
+                b1 += f32x2{yq[sp].x, yq[sp].y};
             }
 #pragma unroll
             for (int sp = 0; sp < kZS; ++sp) bz += zq[sp];
