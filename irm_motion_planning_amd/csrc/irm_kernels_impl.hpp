@@ -1988,12 +1988,15 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         int idx;
     };
     // Latency-hiding load batches (finalize's records and start/goal terms, stage 2's split-K partial
-    // sums, the z unit's operands) hold more values live at once: used for the D = 3, N <= 128 shapes,
-    // where they fit without spills; at N = 256 or D = 7 they pushed the spill-free GD single-loop
-    // variants into scratch (C5: 14 spilled VGPRs)
-    constexpr bool kLat = D <= 3 && S::kNW > 0 && S::NK <= 128;
+    // sums, the z unit's operands) hold more values live at once: stage 2's and the z unit's only for
+    // N <= 128, where they fit without spills; at N = 256 (four splits, eight z ranges) they pushed the
+    // spill-free GD single-loop variants into scratch (C5: 14 spilled VGPRs)
+    // finalize's batch: fixed shapes with one waypoint per lane (C4's two-waypoints-per-lane kernel, one
+    // wave record per trajectory, measured 2 % slower with it; C5 / C7 1.5-2 % faster)
+    constexpr bool kLatF = S::kNW > 0 && WPL == 1;
+    constexpr bool kLatS = S::kNW > 0 && S::NK <= 128;   // stage 2's and the z unit's: N <= 128
     auto finalize = [&](float lsg_e) {
-        if constexpr (!kLat) {
+        if constexpr (!kLatF) {
             const float* r0 = red + (t * WPTL) * 8;
             float cmax = r0[0];
             int cidx = __float_as_int(r0[1]);
@@ -2184,7 +2187,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 a[i] = ap[(size_t)i * 64];
                 bb[i] = *reinterpret_cast<const f32x4*>(el + (sp * KQZ + i) * 16);
             }
-            if constexpr (kLat) __builtin_amdgcn_sched_barrier(0);  // all loads in flight before the first MFMA
+            if constexpr (kLatS) __builtin_amdgcn_sched_barrier(0);  // all loads in flight before the first MFMA
             f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int i = 0; i < KQZ; ++i) {
@@ -2223,7 +2226,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // accumulation order per tile as the general form below)
     constexpr int kMTG = S::NK / 16, kGT = (kMTG + MAXT / 64 - 1) / (MAXT / 64);
     constexpr bool kS2Fix = FULL && S::kNW > 0;
-    constexpr bool kS2Batch = kS2Fix && kLat;  // stage 2's partial sums read in one batch
+    constexpr bool kS2Batch = kS2Fix && kLatS;  // stage 2's partial sums read in one batch
     auto stage2 = [&]() {
         f32x4 acc[S2T];
 #pragma unroll
