@@ -1034,15 +1034,32 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
     // stage 1 over the units of this wave: Ypart[s] = Fᵀ·[a'; b'] (velocity half if `full`)
     auto stage1 = [&](bool full) {
         const float* xl = X + (lane >> 4) * kLd + (lane & 15);
+        // QB k-quads per batch: their operator fragments (L2) and B rows (LDS) in flight together, then
+        // the MFMAs in the sequential order (dense / large-N operators; the REGOPS shapes keep QB = 1)
         auto quads = [&](const f32x4* ap, int qoff, int k0, int k1, f32x4& acc0, f32x4& acc1) {
-            for (int kq = k0; kq < k1; ++kq) {
-                const f32x4 a = ap[(size_t)kq * 64];
-                const float* xb = xl + (qoff + kq) * 16 * kLd;
-                const float b0 = xb[0], b1 = xb[4 * kLd], b2 = xb[8 * kLd], b3 = xb[12 * kLd];
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b0, acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b1, acc1, 0, 0, 0);
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b2, acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b3, acc1, 0, 0, 0);
+            constexpr int QB = REGOPS ? 1 : 4;
+            for (int kq = k0; kq < k1; kq += QB) {
+                f32x4 a[QB];
+                float bq[QB][4];
+#pragma unroll
+                for (int j = 0; j < QB; ++j) {
+                    const bool in = kq + j < k1;
+                    const float* xb = xl + (qoff + kq + j) * 16 * kLd;
+                    a[j] = in ? ap[(size_t)(kq + j) * 64] : f32x4{0.f, 0.f, 0.f, 0.f};
+                    bq[j][0] = in ? xb[0] : 0.f;
+                    bq[j][1] = in ? xb[4 * kLd] : 0.f;
+                    bq[j][2] = in ? xb[8 * kLd] : 0.f;
+                    bq[j][3] = in ? xb[12 * kLd] : 0.f;
+                }
+#pragma unroll
+                for (int j = 0; j < QB; ++j) {
+                    if (kq + j < k1) {
+                        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][0], bq[j][0], acc0, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][1], bq[j][1], acc1, 0, 0, 0);
+                        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][2], bq[j][2], acc0, 0, 0, 0);
+                        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j][3], bq[j][3], acc1, 0, 0, 0);
+                    }
+                }
             }
         };
         if (REGOPS) {  // one unit per wave (regops_fit), position-half fragments in VGPRs
@@ -1203,6 +1220,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
             IRM_STAMP(2);
             // stage 2: G tiles; GD also dP = F(MP × RP)·Σ_s Ypart[s], only the direction columns
             {
+                constexpr int kTG = REGOPS ? 1 : 4;  // L2-operand tiles per pass (dense / large-N operators)
                 const float* xl = Ypart + (lane >> 4) * kLd + (lane & 15);
                 // y' rows (+ GD: z, the folded rounding residual, for the F tiles)
                 auto bload = [&](int i, float& b0, float& b1, float& b2, float& b3, bool withz = true) {
@@ -1226,19 +1244,35 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                     // G tiles: (V_R·y')[waypoint] into X's position rows (X was consumed by stage 1;
                     // only the direction columns are written; every evaluation round rewrites X), from the
                     // top wave down
-                    for (int u = nwaves - 1 - wave; u < KQa; u += nwaves) {
-                        const f32x4* ap = reinterpret_cast<const f32x4*>(P.VNs) + (size_t)u * KQ2 * 64 + lane;
-                        f32x4 c0 = {0.f, 0.f, 0.f, 0.f};
+                    // up to kTG tiles per pass over the k-quads: one B read shared by the pass's tiles and
+                    // their A fragments in flight together (each tile's accumulation order unchanged)
+                    for (int u0 = nwaves - 1 - wave; u0 < KQa; u0 += kTG * nwaves) {
+                        f32x4 c[kTG];
+#pragma unroll
+                        for (int g = 0; g < kTG; ++g) c[g] = f32x4{0.f, 0.f, 0.f, 0.f};
                         for (int i = 0; i < KQ2; ++i) {
                             float b0, b1, b2, b3;
                             bload(i, b0, b1, b2, b3, false);
-                            const f32x4 a = ap[(size_t)i * 64];
-                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b0, c0, 0, 0, 0);
-                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b1, c0, 0, 0, 0);
-                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b2, c0, 0, 0, 0);
-                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b3, c0, 0, 0, 0);
+                            f32x4 a[kTG];
+#pragma unroll
+                            for (int g = 0; g < kTG; ++g) {
+                                const int u = u0 + g * nwaves;
+                                a[g] = u < KQa ? reinterpret_cast<const f32x4*>(P.VNs)[((size_t)u * KQ2 + i) * 64 + lane]
+                                               : f32x4{0.f, 0.f, 0.f, 0.f};
+                            }
+#pragma unroll
+                            for (int g = 0; g < kTG; ++g) {
+                                if (u0 + g * nwaves < KQa) {
+                                    c[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[g][0], b0, c[g], 0, 0, 0);
+                                    c[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[g][1], b1, c[g], 0, 0, 0);
+                                    c[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[g][2], b2, c[g], 0, 0, 0);
+                                    c[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[g][3], b3, c[g], 0, 0, 0);
+                                }
+                            }
                         }
-                        store_tile(X, u, c0, dirmask);
+#pragma unroll
+                        for (int g = 0; g < kTG; ++g)
+                            if (u0 + g * nwaves < KQa) store_tile(X, u0 + g * nwaves, c[g], dirmask);
                     }
                 }
                 if constexpr (BLS) {
@@ -1270,19 +1304,33 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                     for (int j = 0; j < S2T; ++j)
                         if (wave + j * nwaves < MT2) store_tile(dP, wave + j * nwaves, acc[j], dirmask);
                 } else {
-                    for (int tile = wave; tile < MT2; tile += nwaves) {
-                        f32x4 c0 = {0.f, 0.f, 0.f, 0.f};
-                        const f32x4* ap = reinterpret_cast<const f32x4*>(F2) + ((size_t)tile * KQ2) * 64 + lane;
+                    for (int t0 = wave; t0 < MT2; t0 += kTG * nwaves) {  // kTG tiles per pass, as above
+                        f32x4 c[kTG];
+#pragma unroll
+                        for (int g = 0; g < kTG; ++g) c[g] = f32x4{0.f, 0.f, 0.f, 0.f};
                         for (int i = 0; i < KQ2; ++i) {
                             float b0, b1, b2, b3;
                             bload(i, b0, b1, b2, b3);
-                            const f32x4 a = ap[(size_t)i * 64];
-                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b0, c0, 0, 0, 0);
-                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b1, c0, 0, 0, 0);
-                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b2, c0, 0, 0, 0);
-                            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b3, c0, 0, 0, 0);
+                            f32x4 a[kTG];
+#pragma unroll
+                            for (int g = 0; g < kTG; ++g) {
+                                const int tile = t0 + g * nwaves;
+                                a[g] = tile < MT2 ? reinterpret_cast<const f32x4*>(F2)[((size_t)tile * KQ2 + i) * 64 + lane]
+                                                  : f32x4{0.f, 0.f, 0.f, 0.f};
+                            }
+#pragma unroll
+                            for (int g = 0; g < kTG; ++g) {
+                                if (t0 + g * nwaves < MT2) {
+                                    c[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[g][0], b0, c[g], 0, 0, 0);
+                                    c[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[g][1], b1, c[g], 0, 0, 0);
+                                    c[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[g][2], b2, c[g], 0, 0, 0);
+                                    c[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[g][3], b3, c[g], 0, 0, 0);
+                                }
+                            }
                         }
-                        store_tile(dP, tile, c0, dirmask);
+#pragma unroll
+                        for (int g = 0; g < kTG; ++g)
+                            if (t0 + g * nwaves < MT2) store_tile(dP, t0 + g * nwaves, c[g], dirmask);
                     }
                 }
             }

@@ -57,5 +57,6 @@ def run(cfg, tb=0, rank=0, faithful=False):
 
 
 if __name__ == "__main__":
-    for cfg in sys.argv[1:] or ["c3", "c2", "c5"]:
-        run(cfg)
+    for cfg in sys.argv[1:] or ["c3", "c2", "c5"]:  # "c5@-1": config at --operator-rank -1 (dense)
+        name, _, rank = cfg.partition("@")
+        run(name, rank=int(rank) if rank else 0)

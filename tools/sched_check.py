@@ -27,13 +27,15 @@ CASES = [  # (name, config, faithful, batch, general kernel, optimizer override)
     ("c5_bench_general", "c5", False, 32, True, None),
     ("c7_faithful", "c7", True, 64, False, None),
     ("c7_bls", "c7", True, 16, False, "bls"),
+    ("c5_dense", "c5", False, 32, False, None, -1),  # (operator rank) k_optimize at R = N, L2 operands
+    ("c3_dense_faithful", "c3", True, 32, False, None, -1),
 ]
 
 
 def run(out):
     res = {}
     only = os.environ.get("IRM_CASES")
-    for name, cfg, faithful, B, general, opt in CASES:
+    for name, cfg, faithful, B, general, opt, *rank in CASES:
         if only and name not in only.split(","):
             continue
         args = bench.make_args(cfg, faithful, 200)
@@ -43,7 +45,7 @@ def run(out):
         if general:
             os.environ["IRM_GENERAL_KERNEL"] = "1"
         try:
-            c = Context(params_from_args(args))
+            c = Context(params_from_args(args, operator_rank=rank[0]) if rank else params_from_args(args))
         finally:
             os.environ.pop("IRM_GENERAL_KERNEL", None)
         alpha, traj, st = c.optimize(s[:B], g[:B], obs)
