@@ -678,6 +678,7 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
     kp.NK = NK;
     kp.MP = MP;
     kp.RP = RP;
+    kp.v_ident = p->operator_rank < 0 ? 1 : 0;
     kp.O = 0;
     kp.optimizer = p->optimizer;
     kp.max_inner = p->max_inner_iteration;

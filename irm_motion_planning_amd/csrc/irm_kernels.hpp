@@ -38,6 +38,7 @@ struct KParams {
     int32_t BT;          // threads per workgroup = TB·NW
     int32_t nsplit;      // stage-1 split-K factor
     int32_t regops;      // operator A-fragments held in VGPRs (k_optimize<…, REGOPS>)
+    int32_t v_ident;     // V_R = I (dense operator, --operator-rank -1): G = y'' rows, no G-tile MFMAs
     // optimiser
     int32_t optimizer, max_inner, max_outer, max_bls, cvdl, record_series, max_series;
     int32_t lean_ok;  // k_gd_single may serve GD single-loop launches (IRM_GENERAL_KERNEL=1 clears it)

@@ -1244,6 +1244,19 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                     // G tiles: (V_R·y')[waypoint] into X's position rows (X was consumed by stage 1;
                     // only the direction columns are written; every evaluation round rewrites X), from the
                     // top wave down
+                    // dense operator (V_R = I): tile u of V_R·y' is y' rows u·16.. themselves — the MFMA's
+                    // 1·y + exact zeros, i.e. the partial sums from +0 (bload's order): no operator loads
+                    if (P.v_ident) {
+                        for (int u = nwaves - 1 - wave; u < KQa; u += nwaves) {
+                            const float* yr = Ypart + (u * 16 + 4 * (lane >> 4)) * kLd + (lane & 15);
+                            f32x4 c0 = {0.f, 0.f, 0.f, 0.f};
+                            for (int sp = 0; sp < nsplit; ++sp) {
+#pragma unroll
+                                for (int i = 0; i < 4; ++i) c0[i] += yr[(sp * RP + i) * kLd];
+                            }
+                            store_tile(X, u, c0, dirmask);
+                        }
+                    } else
                     // up to kTG tiles per pass over the k-quads: one B read shared by the pass's tiles and
                     // their A fragments in flight together (each tile's accumulation order unchanged)
                     for (int u0 = nwaves - 1 - wave; u0 < KQa; u0 += kTG * nwaves) {
@@ -3176,6 +3189,7 @@ hipError_t launch_general_shape(const KParams& p, hipStream_t s, LaunchDesc* des
             desc->flow = optimizer_flow(p);
             desc->wpl = 1;
             desc->rank_z = desc->rank_dir = desc->rank_g = p.RP;
+            if (p.v_ident) desc->rank_g = 0;  // V_R = I: G is y'' itself (no G-tile MFMAs)
         };
         auto go = [&](auto bc) {
             constexpr bool BB = decltype(bc)::value;
