@@ -236,7 +236,7 @@ typedef struct irm_launch_plan {
     int32_t grid;               /* workgroups                                              */
     int32_t lds_bytes;          /* per workgroup                                           */
     int32_t traj_per_block;
-    int32_t rank_z;             /* operator rank of the rounding-residual projection       */
+    int32_t rank_z;             /* operator rank of the rounding-residual projection (0: V_R = I) */
     int32_t rank_dir;           /* ... of the waypoint direction F·y''                     */
     int32_t rank_g;             /* ... of the α-space gradient G = V_R·y'' (0: V_R = I, a copy) */
     float lam16;                /* λ_16/λ_0 of [K; dK]ᵀ[K; dK] as built (0: not in the operator) */

@@ -1171,6 +1171,16 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                 // into Ymix, one unit per r-tile over all k-quads, operator from L2 — added to y' for
                 // stage 2's F tiles, i.e. [T; V] += L·e·J one step late (k_lean's scheme)
                 const float* xl = dP + (lane >> 4) * kLd + (lane & 15);
+                // V_R = I (dense operator): z is e' itself (the MFMA's 1·e' plus exact zeros, from +0)
+                if (P.v_ident) {
+                    for (int u = nwaves - 1 - wave; u < MT1; u += nwaves) {
+                        const float* er = dP + (u * 16 + 4 * (lane >> 4)) * kLd + (lane & 15);
+                        f32x4 c0;
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) c0[i] = 0.f + er[i * kLd];
+                        store_tile(Ymix, u, c0, 0xFFFFu);
+                    }
+                } else
                 for (int u = nwaves - 1 - wave; u < MT1; u += nwaves) {
                     const f32x4* ap = reinterpret_cast<const f32x4*>(P.VTs) + (size_t)u * KQa * 64 + lane;
                     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -3189,7 +3199,7 @@ hipError_t launch_general_shape(const KParams& p, hipStream_t s, LaunchDesc* des
             desc->flow = optimizer_flow(p);
             desc->wpl = 1;
             desc->rank_z = desc->rank_dir = desc->rank_g = p.RP;
-            if (p.v_ident) desc->rank_g = 0;  // V_R = I: G is y'' itself (no G-tile MFMAs)
+            if (p.v_ident) desc->rank_g = desc->rank_z = 0;  // V_R = I: G is y'', z is e' (no MFMAs)
         };
         auto go = [&](auto bc) {
             constexpr bool BB = decltype(bc)::value;

@@ -442,15 +442,15 @@ def test_launch_plan_names_the_dispatched_kernel(cfg, faithful, B, want):
 
 def test_dense_operator_plan_skips_identity_g_tiles():
     """--operator-rank -1 (F = L, V_R = I): the general kernel at R = N forms G = V_R·y'' as the y'' rows
-    themselves (no G-tile MFMAs), and the plan says so (rank_g 0), so bench's executed-flop count
-    excludes them."""
+    themselves and z = V_Rᵀ·e' as e' (no MFMAs on the identity), and the plan says so (rank_g = rank_z
+    = 0), so bench's executed-flop count excludes them."""
     import bench
     from irm_motion_planning_amd.context import Context
     from irm_motion_planning_amd.params import params_from_args
     c = Context(params_from_args(bench.make_args("c5", False, 200), operator_rank=-1))
     pl = c.launch_plan(512, bench.CONFIGS["c5"][4])
     assert pl["kernel"].startswith("k_optimize") and not pl["lean"], pl
-    assert (pl["rank_z"], pl["rank_dir"], pl["rank_g"]) == (256, 256, 0), pl
+    assert (pl["rank_z"], pl["rank_dir"], pl["rank_g"]) == (0, 256, 0), pl
 
 
 @pytest.mark.parametrize("sigma,rank", [(0.07, 0), (0.1, 32)])
