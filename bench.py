@@ -283,6 +283,18 @@ def aggregate(elapsed, iters_rank, world, device):
     return float(t.item()), float(it.item())
 
 
+def rank_values(x, world, device):
+    """x of every rank, in rank order (all_gather of one float64)."""
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    if world == 1:
+        return [float(x)]
+    import torch.distributed as dist
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [float(v.item()) for v in out]
+
+
 def dry_run(a, world, rank):
     """The multi-rank plumbing of main() without the device: shard, environment broadcast, the
     max-time / Σ-iterations reduction.  Prints the JSON line with value null."""
@@ -345,6 +357,16 @@ def main():
     gloo = a.dist_backend == "gloo"
     if gloo:  # rehearsal: ranks may outnumber the GPUs of the box (counting devices does not init HIP)
         local = local % max(1, torch.cuda.device_count())
+    desc, B, N, D, O, opt = CONFIGS[a.config]
+    args = make_args(a.config, a.faithful, a.max_inner)
+    start, goal, obstacles = make_problem(a.config, world, rank)
+    # The CPU baselines run first, before this process touches the GPU — and, at world > 1, before the
+    # process group exists: init_process_group("nccl", device_id=…) forms the RCCL communicator
+    # eagerly, which initialises HIP on the device, and the batched baseline forks worker processes.
+    # The other ranks wait for rank 0 in the rendezvous meanwhile.
+    cpu = None
+    if rank == 0 and not a.no_cpu_baseline and not a.dry_run:
+        cpu = cpu_baseline(a.config, args, start, goal, obstacles)
     if world > 1:
         if gloo or a.dry_run:
             dist.init_process_group("gloo")
@@ -352,11 +374,6 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if a.dry_run:
         return dry_run(a, world, rank)
-    desc, B, N, D, O, opt = CONFIGS[a.config]
-    args = make_args(a.config, a.faithful, a.max_inner)
-    start, goal, obstacles = make_problem(a.config, world, rank)
-    # the CPU baselines run first, before this process touches the GPU (the batched one forks workers)
-    cpu = cpu_baseline(a.config, args, start, goal, obstacles) if rank == 0 and not a.no_cpu_baseline else None
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -406,6 +423,8 @@ def main():
     trials_rank = float(st[:, 4].sum())  # BLS line-search trials (one evaluation round each)
     elapsed_max, iters_all = aggregate(elapsed, iters_rank, world, cdev)
     value = iters_all * a.steps / elapsed_max
+    kernel_ms_ranks = rank_values(kernel_ms, world, cdev)  # what each rank's launches took
+    world_seen = dist.get_world_size() if world > 1 else 1  # the ranks the collectives ran over
 
     plan = ctx.launch_plan(B, O)
     kernel = plan_label(plan)
@@ -424,6 +443,7 @@ def main():
         "value": value,
         "unit": "iterations/s",
         "n_gpus": world,
+        "world_size": world_seen,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": 1000 * elapsed_max / a.steps,
@@ -446,6 +466,7 @@ def main():
             "traffic_source": traffic_src,
             "kernel": kernel,
             "kernel_ms": kernel_ms,
+            "kernel_ms_per_rank": kernel_ms_ranks,
             "flops_per_iteration": exec_f,
             "flops_per_launch": launch_flops,
             "bls_trials_per_launch": trials_rank if opt == "bls" else None,

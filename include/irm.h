@@ -224,9 +224,12 @@ int irm_optimize_batch_dev(irm_ctx* ctx, const irm_batch_dev* args, void* stream
 int32_t irm_series_capacity(const irm_ctx* ctx);
 
 /* The optimiser launch that irm_optimize_batch(_dev) runs for `batch` problems with n_obstacles
- * obstacles (record_series: series_out passed).  Filled in by the launch dispatch itself with
- * nothing launched, so it names the kernel that actually runs (bench.py's flop model and kernel
- * label come from here).  ABI 3; no reference counterpart. */
+ * obstacles (record_series: series_out passed; the context's own irm_params.record_series counts
+ * too, as in the launch).  Filled in by the launch dispatch itself with nothing launched, so it
+ * names the kernel that actually runs (bench.py's flop model and kernel label come from here).
+ * The plan assumes one obstacle table shared by the batch (obstacle_stride 0): per-problem tables
+ * take more LDS per workgroup and may run fewer trajectories per workgroup.  ABI 3; no reference
+ * counterpart. */
 typedef struct irm_launch_plan {
     char kernel[128];           /* template instance, e.g. k_lean<FixShape<3,128,32>,512,1,FULL,GD1> */
     int32_t lean;               /* 1: k_lean, 0: k_optimize                                */
@@ -245,8 +248,9 @@ typedef struct irm_launch_plan {
 int irm_optimize_plan(const irm_ctx* ctx, int32_t batch, int32_t n_obstacles, int32_t record_series,
                       irm_launch_plan* out);
 
-/* Source hash the library was built from: the first 16 hex digits of the SHA-256 over
- * every file of irm_motion_planning_amd/csrc and include/irm.h (build.py); "unknown" otherwise.
+/* Build id of the library: the first 16 hex digits of the SHA-256 over every file of
+ * irm_motion_planning_amd/csrc and include/irm.h, the compile flags of every unit and the build
+ * variant (build.py source_hash); "unknown" otherwise.
  * __graft_entry__.smoke() compares it with the checked-out sources.  ABI 3. */
 const char* irm_build_id(void);
 

@@ -25,8 +25,14 @@ HEADERS = [os.path.join(CSRC, h) for h in ("irm_kernels.hpp", "irm_kernels_impl.
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 # -amdgpu-atomic-optimizer-strategy=None: every LDS atomic in the kernels is issued by one lane (flag
-# words); the optimizer's scan over the active lanes is a ~25-instruction waterfall per round there
+# words); the optimizer's scan over the active lanes is a ~25-instruction waterfall per round there.
+# -ffp-contract=off: no fused multiply-add the source does not write (fmaf / pkfma) — the results do
+# not depend on the compiler's contraction choices, which moved with unrelated code before (round 3).
+# -fno-slp-vectorize: no packing of scalar f32 arithmetic into v_pk_* (the explicit f32x2 code of the
+# obstacle potential stays packed): the packed forms needed v_mov pairs around them and measured
+# slower (C3 0.763 -> 0.726 ms, same box, profiles/r04_*).
 CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno-unused-function",
+          "-ffp-contract=off", "-fno-slp-vectorize",
           "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
 FIX_SHAPES = [(3, 50), (3, 64), (3, 128), (3, 256), (7, 128), (7, 256)]  # IRM_FIX_SHAPES in irm_kernels_impl.hpp
 MAX_D = 8
@@ -51,10 +57,12 @@ def source_files():
     return sorted(glob.glob(os.path.join(CSRC, "*"))) + [os.path.normpath(os.path.join(HERE, "..", "include", "irm.h"))]
 
 
-def source_hash():
+def source_hash(variant=""):
     """First 16 hex digits of the SHA-256 over the sources (names relative to the repo root, then
-    contents).  irm_build_id() of a library built here returns it (-DIRM_SOURCE_HASH on irm_host.cpp);
-    __graft_entry__.smoke() compares the two, so a stale prebuilt library fails."""
+    contents), the compile flags of every unit and the variant's name and extra flags.  irm_build_id()
+    of a library built here returns it (-DIRM_SOURCE_HASH on irm_host.cpp); __graft_entry__.smoke()
+    compares the two, so a stale prebuilt library — or one built with other flags (a profiling or
+    experimental variant) — fails."""
     root = os.path.normpath(os.path.join(HERE, ".."))
     h = hashlib.sha256()
     for f in source_files():
@@ -62,13 +70,26 @@ def source_hash():
         with open(f, "rb") as fh:
             h.update(fh.read())
         h.update(b"\0")
+    name, extra = variant_spec(variant)
+    h.update(("\0".join([name] + CFLAGS + extra) + "\0").encode())
+    for oname, src, flags in _units():
+        h.update(("\0".join([oname, src] + flags) + "\0").encode())
     return h.hexdigest()[:16]
 
 
-def units():
-    """(object name, source, extra flags) of every compilation unit."""
-    u = [("irm_kernels", "irm_kernels.hip", []),
-         ("irm_host", "irm_host.cpp", [f'-DIRM_SOURCE_HASH="{source_hash()}"'])]
+def variant_spec(variant):
+    """(library file name, extra flags) of a build variant: the named ones of VARIANTS, or an ad-hoc
+    experiment registered by add_variant (same-box A/B builds, tools/gpu/*.sh)."""
+    return VARIANTS[variant]
+
+
+def add_variant(name, flags):
+    VARIANTS[name] = (f"libirm_hip_{name}.so", list(flags))
+
+
+def _units():
+    """(object name, source, extra flags) of every compilation unit, before the build id."""
+    u = [("irm_kernels", "irm_kernels.hip", []), ("irm_host", "irm_host.cpp", [])]
     # (DynShape units keep the default scheduler: with iterative-ILP the D = 5 register-resident
     # variant, which spills heavily, left the exact-iteration band — tests/test_gpu_parity.py::
     # test_generic_shapes_match_reference_iteration[64-5] — so it is not used there)
@@ -80,6 +101,12 @@ def units():
     return u
 
 
+def units(variant=""):
+    """(object name, source, extra flags) of every compilation unit (irm_host carries the build id)."""
+    bid = f'-DIRM_SOURCE_HASH="{source_hash(variant)}"'
+    return [(o, src, fl + [bid] if o == "irm_host" else fl) for o, src, fl in _units()]
+
+
 def _newer(target, deps):
     if not os.path.exists(target):
         return True
@@ -88,13 +115,19 @@ def _newer(target, deps):
 
 
 def build(force=False, verbose=False, variant="", jobs=None):
-    name, extra = VARIANTS[variant]
+    name, extra = variant_spec(variant)
     out = os.path.join(HERE, name)
     odir = os.path.join(OBJ, variant or "release")
     os.makedirs(odir, exist_ok=True)
     jobs = jobs or min(16, os.cpu_count() or 1)
     todo, objs = [], []
-    for oname, src, flags in units():
+    stamp = os.path.join(odir, "flags.txt")  # a change of flags rebuilds every object
+    flagtxt = "\n".join(CFLAGS + extra)
+    if not os.path.exists(stamp) or open(stamp).read() != flagtxt:
+        force = True
+        with open(stamp, "w") as fh:
+            fh.write(flagtxt)
+    for oname, src, flags in units(variant):
         obj = os.path.join(odir, oname + ".o")
         objs.append(obj)
         deps = [os.path.join(CSRC, src), __file__] + HEADERS
@@ -130,13 +163,20 @@ def build(force=False, verbose=False, variant="", jobs=None):
 def asm(out_dir, inst=("-DIRM_INST_FIX_D=3", "-DIRM_INST_FIX_N=128")):
     """Emit the gfx950 assembly of one instantiation unit (for ISA inspection)."""
     os.makedirs(out_dir, exist_ok=True)
-    cmd = [HIPCC, "-O3", "-std=c++17", f"--offload-arch={ARCH}", "--cuda-device-only", "-S", *inst,
+    cmd = [HIPCC] + [f for f in CFLAGS if f != "-fPIC"] + ["--cuda-device-only", "-S", *inst,
            "-o", os.path.join(out_dir, "irm_opt.s"), os.path.join(CSRC, "irm_opt_inst.hip")]
     subprocess.check_call(cmd, cwd=CSRC)
 
 
 if __name__ == "__main__":
     jobs = int(sys.argv[sys.argv.index("-j") + 1]) if "-j" in sys.argv else None
+    if "--variant" in sys.argv:  # ad-hoc experiment: --variant NAME [--extra "FLAGS"]
+        vname = sys.argv[sys.argv.index("--variant") + 1]
+        vflags = sys.argv[sys.argv.index("--extra") + 1].split() if "--extra" in sys.argv else []
+        add_variant(vname, vflags)
+        build(force="--force" in sys.argv, variant=vname, verbose=False, jobs=jobs)
+        print("built", VARIANTS[vname][0], source_hash(vname))
+        sys.exit(0)
     build(force="--force" in sys.argv, verbose=True, jobs=jobs)
     for v in VARIANTS:  # e.g. --defsched (tools/sched_check.py)
         if v and v != "prof" and f"--{v}" in sys.argv:

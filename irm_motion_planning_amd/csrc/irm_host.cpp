@@ -696,9 +696,11 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
     // GD weight decay (1 − λ_reg·lr) per outer iteration, in fp32 as the reference evaluates it:
     // lr = dual_lr[k] is an fp32 array element (optimizer_GD.py:38-39, :209) and the Python float
     // λ_reg enters weakly typed, so both the product and the difference round to fp32
-    // (optimizer_GD.py:81, :185) — two statements, so that the host compiler cannot fuse them
+    // (optimizer_GD.py:81, :185).  The product is rounded through a volatile: clang contracts across
+    // statements under -ffp-contract=fast, so only the missing FMA of the default host target kept the
+    // two roundings apart before (a -march with FMA would have fused them into one)
     for (int i = 0; i < IRM_MAX_LR; ++i) {
-        const float prod = p->lambda_reg * p->gd_lr[i];
+        volatile float prod = p->lambda_reg * p->gd_lr[i];
         kp.gd_c[i] = 1.f - prod;
     }
     kp.bls_lr0 = p->bls_lr_start;
@@ -1156,7 +1158,9 @@ int irm_optimize_plan(const irm_ctx* c, int32_t batch, int32_t n_obstacles, int3
     KParams kp = c->kp;
     kp.B = batch;
     kp.O = n_obstacles;
-    kp.record_series = record_series ? 1 : 0;
+    // the series flow runs when the context records it (irm_params.record_series) or the call asks
+    // for the series (irm_optimize_batch with series_out) — as in irm_optimize_batch(_dev)
+    kp.record_series = (c->kp.record_series || record_series) ? 1 : 0;
     if (choose_shape(c, batch, true, kp, nullptr) <= 0) return fail(IRM_EINVAL, "no workgroup shape fits LDS");
     irm::LaunchDesc d{};
     d.describe_only = true;

@@ -36,6 +36,10 @@ namespace irm {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// The kernels are compiled with -ffp-contract=off (build.py): every fused multiply-add is written
+// as one, so the arithmetic does not depend on the compiler's contraction choices.
+__device__ __forceinline__ f32x2 pkfma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 // ------------------------------------------------------------ LDS planning
 
 // ------------------------------------------------------------ wave helpers
@@ -243,8 +247,8 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         const float sn = snv[d], cs = csv[d];
-        fx += P.link[d] * cs;
-        fy += P.link[d] * sn;
+        fx = fmaf(P.link[d], cs, fx);
+        fy = fmaf(P.link[d], sn, fy);
         px[d] = fx;
         py[d] = fy;
         xs[d] = -(P.link[d] * sn);
@@ -265,12 +269,12 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
         const f32x2 fx2 = {x, x}, fy2 = {y, y}, one = {1.f, 1.f};
         auto pair2 = [&](f32x2 ox, f32x2 oy) {
             const f32x2 dx = fx2 - ox, dy = fy2 - oy;
-            const f32x2 e = dy * dy + (dx * dx + one);
+            const f32x2 e = pkfma(dy, dy, pkfma(dx, dx, one));
             const f32x2 u = {__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
             cv2 += u;
             const f32x2 u2 = u * u;
-            ax2 += dx * u2;
-            ay2 += dy * u2;
+            ax2 = pkfma(dx, u2, ax2);
+            ay2 = pkfma(dy, u2, ay2);
         };
 #ifdef IRM_X_NOOBS
         if (false) {
@@ -284,15 +288,15 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
                 const f32x4 p = oreg ? oreg[i] : o4[i];
                 dx[i] = fx2 - p.xy;
                 dy[i] = fy2 - p.zw;
-                const f32x2 e = dy[i] * dy[i] + (dx[i] * dx[i] + one);
+                const f32x2 e = pkfma(dy[i], dy[i], pkfma(dx[i], dx[i], one));
                 u[i] = f32x2{__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
             }
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 cv2 += u[i];
                 const f32x2 u2 = u[i] * u[i];
-                ax2 += dx[i] * u2;
-                ay2 += dy[i] * u2;
+                ax2 = pkfma(dx[i], u2, ax2);
+                ay2 = pkfma(dy[i], u2, ay2);
             }
         } else {
             for (int c = 0; c < nq; ++c) {
@@ -333,7 +337,7 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
         for (int l = D - 1; l >= 0; --l) {
             GX += gxj[l];
             GY += gyj[l];
-            acc += xs[l] * GX + ys[l] * GY;
+            acc = fmaf(xs[l], GX, fmaf(ys[l], GY, acc));
             w.jx[l] = acc;
             w.jy[l] = 0.f;
         }
@@ -373,12 +377,12 @@ __device__ __forceinline__ void potential_pair(const KParams& P, const float* __
     const f32x2 one = {1.f, 1.f};
     auto pair2 = [&](const f32x2& fx2, const f32x2& fy2, f32x2 ox, f32x2 oy, f32x2& cv2, f32x2& ax2, f32x2& ay2) {
         const f32x2 dx = fx2 - ox, dy = fy2 - oy;
-        const f32x2 e = dy * dy + (dx * dx + one);
+        const f32x2 e = pkfma(dy, dy, pkfma(dx, dx, one));
         const f32x2 u = {__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
         cv2 += u;
         const f32x2 u2 = u * u;
-        ax2 += dx * u2;
-        ay2 += dy * u2;
+        ax2 = pkfma(dx, u2, ax2);
+        ay2 = pkfma(dy, u2, ay2);
     };
     for (int c = 0; c < nq; ++c) {
         const f32x4 p0 = o4[2 * c], p1 = o4[2 * c + 1];
@@ -429,8 +433,8 @@ __device__ __forceinline__ void grad_waypoint(const KParams& P, const WP<D>& w, 
         if (!P.cvdl || m) jpg = ((q[d] - P.mean_pos) * P.inv_std2) * P.invN;
         const bool mv = fabsf(v[d]) > P.thr_v;
         if (!P.cvdl || mv) jvg = (v[d] * P.inv_vmax2) * P.invN;
-        a[d] = (wx * w.jx[d] + wy * w.jy[d]) + lsg * sgp + ljl * jpg;
-        b[d] = lsg * sgv + ljl * jvg;
+        a[d] = fmaf(ljl, jpg, fmaf(lsg, sgp, fmaf(wx, w.jx[d], wy * w.jy[d])));
+        b[d] = fmaf(lsg, sgv, ljl * jvg);
     }
 }
 
@@ -452,8 +456,8 @@ __device__ __forceinline__ void grad_waypoint_ep(const KParams& P, const WP<D>& 
         if (!P.cvdl || m) jpg = ((q[d] - P.mean_pos) * P.inv_std2) * P.invN;
         const bool mv = fabsf(v[d]) > P.thr_v;
         if (!P.cvdl || mv) jvg = (v[d] * P.inv_vmax2) * P.invN;
-        a[d] = (wx * w.jx[d] + wy * w.jy[d]) + lsg * sgp + ljl * jpg;
-        b[d] = lsg * sgv + ljl * jvg;
+        a[d] = fmaf(ljl, jpg, fmaf(lsg, sgp, fmaf(wx, w.jx[d], wy * w.jy[d])));
+        b[d] = fmaf(lsg, sgv, ljl * jvg);
     }
 }
 
@@ -1214,9 +1218,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                     for (int k = 0; k < D; ++k) {
                         float m = 0.f;
 #pragma unroll
-                        for (int d = 0; d < D; ++d) m += y[d] * cold[C_MINV + d * D + k];
-                        g2 += y[k] * m;
-                        al += cold[C_WAL + k] * y[k];
+                        for (int d = 0; d < D; ++d) m = fmaf(y[d], cold[C_MINV + d * D + k], m);
+                        g2 = fmaf(y[k], m, g2);
+                        al = fmaf(cold[C_WAL + k], y[k], al);
                     }
                     al = al * al;
                 }
@@ -1466,8 +1470,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
         } else if (phase == PH_GD_INNER) {
 #pragma unroll
             for (int k = 0; k < D; ++k) {
-                q2[k] = cfac * q[k] - step * dT[k];
-                v2[k] = cfac * v[k] - step * dV[k];
+                q2[k] = fmaf(cfac, q[k], -(step * dT[k]));
+                v2[k] = fmaf(cfac, v[k], -(step * dV[k]));
             }
         } else {
 #pragma unroll
@@ -1486,15 +1490,15 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                 else eval_waypoint<D>(P, q2, v2, obs, w);
             }
             IRM_STAMP(8);
-            const float us = P.one_m_lmax * (w.cv * P.invN) + ljl * ((w.jp + w.jv) * P.invN);
+            const float us = fmaf(P.one_m_lmax, w.cv * P.invN, ljl * ((w.jp + w.jv) * P.invN));
             ered_store(valid, w.cv, us, w.tx, w.tn, w.va, phase == PH_RESYNC, n0, red, wave);
             if (valid && (n == 0 || n == N - 1)) {  // trajectory.py:183-204 rows 0 and N−1
                 float a = 0.f, bb = 0.f;
 #pragma unroll
                 for (int d = 0; d < D; ++d) {
                     const float e = q2[d] - (n == 0 ? s[d] : g[d]);
-                    a += e * e;
-                    bb += v2[d] * v2[d];
+                    a = fmaf(e, e, a);
+                    bb = fmaf(v2[d], v2[d], bb);
                 }
                 sg[t * 4 + (n == 0 ? 0 : 2)] = a;
                 sg[t * 4 + (n == 0 ? 1 : 3)] = bb;
@@ -1519,10 +1523,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
             }
             const float e_a0 = sg[t * 4 + 0], e_b0 = sg[t * 4 + 1], e_a1 = sg[t * 4 + 2], e_b1 = sg[t * 4 + 3];
             IRM_STAMP(18);
-            const float sgpc = 0.5f * e_a0 + 0.5f * e_a1;                       // trajectory.py:187
-            const float sgvc = 0.5f * e_b0 + 0.5f * e_b1;                       // trajectory.py:203
+            const float sgpc = fmaf(0.5f, e_a0, 0.5f * e_a1);                   // trajectory.py:187
+            const float sgvc = fmaf(0.5f, e_b0, 0.5f * e_b1);                   // trajectory.py:203
             // trajectory.py:85-87 + 281 (mean and joint-limit terms pre-summed in usum)
-            const float nl = (P.lam_max * cmax + usum) + lsg * (sgpc + sgvc);
+            const float nl = fmaf(lsg, sgpc + sgvc, fmaf(P.lam_max, cmax, usum));
             const float lsg_e = lsg, ljl_e = ljl;
             // --------------------------------------------------- decide
             int accept = 0;
@@ -1637,8 +1641,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
                     float ma = 0.f, mb = 0.f;
 #pragma unroll
                     for (int d = 0; d < D; ++d) {
-                        ma += a[d] * P.JtJ[d * D + k];
-                        mb += bb[d] * P.JtJ[d * D + k];
+                        ma = fmaf(a[d], P.JtJ[d * D + k], ma);
+                        mb = fmaf(bb[d], P.JtJ[d * D + k], mb);
                     }
                     X[n * kLd + t * D + k] = ma;
                     X[(NK + n) * kLd + t * D + k] = mb;
@@ -2023,7 +2027,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         for (int j = 0; j < WPL; ++j) {
             if (WPL == 1 && vl[j]) eval_waypoint<D>(P, q2[j], v2[j], obs, w[j], OREG ? oreg : nullptr);  // oreg: read only when nq == 3
             cvs[j] = w[j].cv;
-            const float u = P.one_m_lmax * (w[j].cv * P.invN) + ljl_e * ((w[j].jp + w[j].jv) * P.invN);
+            const float u = fmaf(P.one_m_lmax, w[j].cv * P.invN, ljl_e * ((w[j].jp + w[j].jv) * P.invN));
             if (j == 0) {
                 us = u;
                 tx = w[j].tx;
@@ -2046,8 +2050,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
                 for (int d = 0; d < D; ++d) {
                     const float e = q2[j][d] - tg[j][d];  // tg: s on row 0, g on row N − 1
-                    a += e * e;
-                    bb += v2[j][d] * v2[j][d];
+                    a = fmaf(e, e, a);
+                    bb = fmaf(v2[j][d], v2[j][d], bb);
                 }
                 sg[t * 4 + (n == 0 ? 0 : 2)] = a;
                 sg[t * 4 + (n == 0 ? 1 : 3)] = bb;
@@ -2085,9 +2089,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             f.b0 = sg[t * 4 + 1];
             f.a1 = sg[t * 4 + 2];
             f.b1 = sg[t * 4 + 3];
-            const float sgpc = 0.5f * f.a0 + 0.5f * f.a1;  // trajectory.py:187
-            const float sgvc = 0.5f * f.b0 + 0.5f * f.b1;  // trajectory.py:203
-            f.nl = (P.lam_max * cmax + usum) + lsg_e * (sgpc + sgvc);
+            const float sgpc = fmaf(0.5f, f.a0, 0.5f * f.a1);  // trajectory.py:187
+            const float sgvc = fmaf(0.5f, f.b0, 0.5f * f.b1);  // trajectory.py:203
+            f.nl = fmaf(lsg_e, sgpc + sgvc, fmaf(P.lam_max, cmax, usum));
             f.idx = cidx;
             f.tx = tx;
             f.tn = tn;
@@ -2124,9 +2128,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         f.b0 = sgr[1];
         f.a1 = sgr[2];
         f.b1 = sgr[3];
-        const float sgpc = 0.5f * f.a0 + 0.5f * f.a1;  // trajectory.py:187
-        const float sgvc = 0.5f * f.b0 + 0.5f * f.b1;  // trajectory.py:203
-        f.nl = (P.lam_max * cmax + usum) + lsg_e * (sgpc + sgvc);
+        const float sgpc = fmaf(0.5f, f.a0, 0.5f * f.a1);  // trajectory.py:187
+        const float sgvc = fmaf(0.5f, f.b0, 0.5f * f.b1);  // trajectory.py:203
+        f.nl = fmaf(lsg_e, sgpc + sgvc, fmaf(P.lam_max, cmax, usum));
         f.idx = cidx;
         f.tx = tx;
         f.tn = tn;
@@ -2149,8 +2153,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     float ma = 0.f, mb = 0.f;
 #pragma unroll
                     for (int d = 0; d < D; ++d) {
-                        ma += a[d] * P.J[k * D + d];
-                        mb += bb[d] * P.J[k * D + d];
+                        ma = fmaf(a[d], P.J[k * D + d], ma);
+                        mb = fmaf(bb[d], P.J[k * D + d], mb);
                     }
                     X[(t * D + k) * ldx + swz(n, t * D + k)] = ma;
                     X[(t * D + k) * ldx + NK + swz(n, t * D + k)] = mb;
@@ -2681,8 +2685,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     }
 #pragma unroll
                     for (int k = 0; k < D; ++k) {
-                        q2[j][k] = cj * q[j][k] - stepj * dt[k];
-                        v2[j][k] = cj * v[j][k] - stepj * dv[k];
+                        q2[j][k] = fmaf(cj, q[j][k], -(stepj * dt[k]));
+                        v2[j][k] = fmaf(cj, v[j][k], -(stepj * dv[k]));
                     }
                 } else {
 #pragma unroll
@@ -2858,7 +2862,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                         q[j][k] = q2[j][k];
                         v[j][k] = v2[j][k];
                         if constexpr (BLS) {
-                            pend[j][k] = er + keep * pend[j][k];
+                            pend[j][k] = fmaf(keep, pend[j][k], er);
                             eo[k] = nsr * pend[j][k];
                         } else {
                             eo[k] = er * ne;

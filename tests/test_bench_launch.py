@@ -61,3 +61,33 @@ def test_bls_flop_model_counts_trials():
     e, ref2 = bench.flops_per_iteration(128, 3, 11, 32)
     assert e == d + t and ref == ref2
     assert t == 4 * 128 * 3 + 14 * 128 * 11 + 24 * 128 * 3  # update + obstacle pairs + FK / penalties
+
+
+def test_cpu_baseline_runs_before_process_group_init(monkeypatch):
+    """At world > 1 rank 0 times the CPU baselines before init_process_group: with the nccl backend and
+    a device_id the communicator forms eagerly (HIP initialised on the device), and the batched
+    baseline forks worker processes, which must not happen after that (VERDICT r03 #3)."""
+    import torch.distributed as dist
+
+    sys.path.insert(0, REPO)
+    import bench
+    order = []
+
+    class Stop(Exception):
+        pass
+
+    def fake_init(*a, **k):
+        order.append("init_process_group")
+        raise Stop
+
+    monkeypatch.setattr(bench, "cpu_baseline", lambda *a, **k: order.append("cpu_baseline"))
+    monkeypatch.setattr(dist, "init_process_group", fake_init)
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("LOCAL_RANK", "0")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--config", "c3"])
+    try:
+        bench.main()
+    except Stop:
+        pass
+    assert order == ["cpu_baseline", "init_process_group"], order

@@ -39,6 +39,13 @@ def ctx(*argv, **overrides):
     return _CTX[key]
 
 
+# Problems of the committed fixtures at which the reference's BLAS and exact-matmul runs part at a
+# decision knife edge: C3 problems 8 (k = 1, 2) and 15 (k = 4) in the k-step test, C4
+# problem 7 after 200 steps (the N = 256 run is chaotic by then).  Named, not counted.
+KNIFE_EDGE_PROBLEMS = {"c3": {8, 15}, "c4": set()}
+VIA_XM_PROBLEMS = {"c3": set(), "c4": {7}}
+
+
 @pytest.fixture(scope="module")
 def fx():
     names = ("ref_bench_c3", "ref_bench_c4", "ref_bls_trials", "ref_e2e_r02")
@@ -80,7 +87,9 @@ def test_gd_first_steps_match_reference(fx, cfg):
             assert abs(float(st["final_loss"][b]) - zm["loss_k"][b, i]) <= loss_band(o, zm, b, i), (k, b)
         print(f"{cfg} {k} steps: |traj - ref (BLAS)| max {max(errs):.2e} over {len(errs)} problems")
     print(f"{cfg}: widest band used {widest:.2e}; argmax knife edges {edges}")
-    assert len(edges) <= 3
+    # the problems whose max-cost argmax is a knife edge of the reference's own K@α0 noise (measured
+    # margins 8e-5 / 3e-6 at C3, none at C4): only these may take the exact-matmul reference's band
+    assert {b for _, b, _ in edges} <= KNIFE_EDGE_PROBLEMS[cfg] and len(edges) <= 3, edges
 
 
 @pytest.mark.parametrize("cfg", ["c3", "c4"])
@@ -121,7 +130,7 @@ def test_gd_200_steps_inside_reference_spread(fx, cfg):
             if not res[0][0]:
                 via_xm.append(b)
     print(f"{cfg}: problems inside the exact-matmul reference's band only: {via_xm}")
-    assert len(via_xm) <= 2
+    assert set(via_xm) <= VIA_XM_PROBLEMS[cfg], via_xm
 
 
 @pytest.mark.parametrize("N,kind", BLS_CASES)
@@ -164,7 +173,9 @@ def test_bls_n500_ulp_ensemble_inside_reference_band():
     a0 = e2e_alpha0("bls_n500")
     r = e2e_reference("bls_n500")
     calls = np.concatenate([r[v]["grad_calls"] for v in r]).astype(float)
-    lo, hi = 0.7 * calls.min(), 1.3 * calls.max()
+    # band: the reference ensemble's range widened to the oracle's own spread (76-128) plus a small
+    # margin — tight enough to exclude the one-step-late scheme's 47-67
+    lo, hi = 0.8 * calls.min(), 1.15 * calls.max()
     got = []
     for seed in range(5):
         sgn = np.random.default_rng(100 + seed).choice([-1.0, 1.0], a0.shape).astype(np.float32)
