@@ -225,24 +225,22 @@ __host__ __device__ inline Plan plan_lds(const KParams& p, bool ops_lds, bool op
 }
 
 
-// LDS of the lean GD kernel (k_gd_single) beyond the optimiser head + obstacles (`base`): the
-// endpoint operator columns hL (2·MP), G's endpoint columns hV (2·NK), the V_R fragments (when
-// staged: vlds), the rounding residual rows e' ([column][waypoint], stride NK + 8), its stage-1
-// partials zp ([split][column][r], stride RP + 8) and the gradient rows G ([column][waypoint]).
+// LDS of the lean kernel (k_lean) beyond the optimiser head + obstacles (`base`): the V_R fragments
+// (when staged: vlds), the rounding residual rows e' ([column][waypoint], stride NK + 8), its stage-1
+// partials zp ([split][column][r], stride RP + 8), the gradient rows G ([column][waypoint]) and the
+// compact endpoint velocity rows ep ([trajectory][2][kEpS]) + a zero word.
 // k-splits of k_lean's residual projection z = V_Rᵀ·e' (rank 16: one row tile, see k_lean): twice
 // the stage-1 splits where the LDS allows (vlds shapes: N ≤ 128, D ≤ 3), so the units stay one per wave
 __host__ __device__ constexpr int lean_zsplit(int nsplit, bool vlds) { return vlds ? 2 * nsplit : nsplit; }
 struct LeanX {
-    int hl, hv, vt, vn, eb, zp, gb, total;
+    int vt, vn, eb, zp, gb, ep, ep0, total;
 };
+// compact copy of each trajectory's endpoint velocity rows b'[0], b'[N−1] of X (k_lean): kEpS floats each
+constexpr int kEpS = 8;
 __host__ __device__ constexpr int lean_ld(int NK) { return NK + 8; }
 __host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, int nsplit, bool vlds) {
     LeanX e{};
     int off = base;
-    e.hl = off;
-    off += al4(2 * MP);
-    e.hv = off;
-    off += al4(2 * NK);
     e.vt = e.vn = 0;
     if (vlds) {
         e.vt = off;
@@ -256,6 +254,10 @@ __host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, in
     off += al4(lean_zsplit(nsplit, vlds) * 16 * lean_ldy(RP));
     e.gb = off;
     off += al4(16 * lean_ld(NK));
+    e.ep = off;
+    off += kMaxTraj * 2 * kEpS;
+    e.ep0 = off;  // one zero word (the endpoint MFMA's B for k = 2, 3)
+    off += 4;
     e.total = off;
     return e;
 }

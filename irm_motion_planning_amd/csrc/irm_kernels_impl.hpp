@@ -59,6 +59,18 @@ __device__ __forceinline__ int dppi(int v) {
     static_assert(CTRL == 0xB1 || CTRL == 0x4E || CTRL == 0x141 || CTRL == 0x140, "in-row permutations only");
     return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true);
 }
+// s + (row_bcast:15 of s) in rows 1 and 3 (ROW = 15), s + (row_bcast:31 of s) in rows 2 and 3 (ROW = 31);
+// the other rows keep s.  As one v_add_f32_dpp (the compiler's DPP combine leaves the float add with a
+// partial row mask as a v_mov_b32_dpp + v_add_f32 pair); s_nop 1: the VALU-write → DPP-read hazard.
+template <int ROW>
+__device__ __forceinline__ float bcast_add(float s) {
+    static_assert(ROW == 15 || ROW == 31, "row broadcasts");
+    if constexpr (ROW == 15)
+        asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf" : "+v"(s));
+    else
+        asm volatile("s_nop 1\n\tv_add_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf" : "+v"(s));
+    return s;
+}
 // max of floats that are ≥ +0 or −inf, on their bit patterns (signed-int order = float order there):
 // no NaN canonicalisation, and the DPP move folds into v_max_i32_dpp
 __device__ __forceinline__ float maxpos(float a, float b) {
@@ -176,7 +188,12 @@ __device__ __forceinline__ void store_tile(float* out, int tile, f32x4 acc, unsi
 // split, fma) and the cephes single-precision minimax polynomials on
 // [−π/4, π/4]; ≈1 ulp, branch-free.  |x| > 1e4 rad falls back to sincosf.
 __device__ __forceinline__ void sincos_poly(float x, float& sn, float& cs) {
-    const float kf = rintf(x * 0.636619772f);
+    // k = round(x·2/π) by the 1.5·2²³ shifter: one fma rounds the exact product to an integer (ties to
+    // even), whose low bits are k's two's-complement bits in t's mantissa (|k| < 2²² here); kf = k as a
+    // float.  (rintf(fl(x·2/π)) differs only where x·2/π lies within an ulp of a half-integer — then r
+    // sits at ±π/4 either way, inside the polynomials' accurate range.)
+    const float t = fmaf(x, 0.636619772f, 12582912.0f);
+    const float kf = t - 12582912.0f;
     float r = fmaf(kf, -1.57079637050628662109375f, x);
     r = fmaf(kf, 4.371138828673793e-08f, r);
     r = fmaf(kf, 1.7151245100058819e-15f, r);
@@ -186,7 +203,7 @@ __device__ __forceinline__ void sincos_poly(float x, float& sn, float& cs) {
                           fmaf(-0.5f, z, 1.0f));
     // quadrant q = kf mod 4: swap on odd q, sin negated for q ∈ {2, 3}, cos for q ∈ {1, 2} — the sign
     // flips as bit 1 of q (resp. q + 1) moved to the sign bit (an xor; −x and the flip agree bit for bit)
-    const int qi = (int)kf;
+    const int qi = __float_as_int(t);  // k mod 4 in the low bits
     const float s0 = (qi & 1) ? cp : sp;
     const float c0 = (qi & 1) ? sp : cp;
     sn = __uint_as_float(__float_as_uint(s0) ^ (((unsigned)qi << 30) & 0x80000000u));
@@ -203,10 +220,11 @@ __device__ __forceinline__ void sincos_fast(float x, float& sn, float& cs) {
 template <int D>
 struct WP {
     float cv, gx, gy;        // obstacle potential and its gradient at the end effector
-    float jp, jv;            // masked joint-position / joint-velocity penalty terms
+    float jp, jv;            // masked joint-position / joint-velocity penalty terms (LEAN: Σ zm², Σ zvm²)
     float tx, tn, va;        // max/min joint position, max |joint velocity|
     float jx[D], jy[D];      // end-effector Jacobian row
     float fx, fy;            // end-effector position (eval_waypoint<…, POT = false>: potential not yet added)
+    float zm[D], zvm[D];     // LEAN: masked (q − μ)/σ_q and v/v_max (0 where the limit mask is off)
 };
 
 // robot.py:29-36 (fk), 75-87 (jacobian); environment.py:46-58
@@ -218,7 +236,30 @@ struct WP {
 // returned as w.jx (with w.gx = 1, w.jy = w.gy = 0) so grad_waypoint is shared.
 // POT = false (end-effector cost only): everything but the obstacle potential, whose inputs are left
 // in w.fx / w.fy (potential_pair evaluates two waypoints' potentials in one pass over the obstacles).
-template <int D, bool WHOLE = false, bool POT = true>
+// LEAN evaluations keep zm / zvm for the gradient inputs at D ≤ 3; at D = 7 the 14 values live across
+// the evaluation barrier pushed the spill-free 7-DoF bench kernels into scratch, so the gradient inputs
+// recompute them there (lean_pen: the same arithmetic, the same values)
+template <int D>
+constexpr bool kLeanKeep = D <= 3;
+template <int D>
+__device__ __forceinline__ void lean_pen(const KParams& P, const float (&q)[D], const float (&v)[D], float (&zm)[D],
+                                         float (&zvm)[D]) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const float z = (q[d] - P.mean_pos) * P.inv_std_pos;
+        const bool m = (q[d] > P.thr_hi) || (q[d] < P.thr_lo);
+        const float zv = v[d] * P.inv_vmax;
+        const bool mv = fabsf(v[d]) > P.thr_v;
+        zm[d] = (P.cvdl && !m) ? 0.f : z;
+        zvm[d] = (P.cvdl && !mv) ? 0.f : zv;
+    }
+}
+
+// LEAN (the optimiser kernels): the penalty terms in the form the loss and the gradient inputs share —
+// zm = mask·(q − μ)/σ_q and zvm = mask·v/v_max per joint, w.jp = Σ zm², w.jv = Σ zvm² (the ½ and the
+// 1/N of trajectory.py:215-227, 245-255 go into the per-trajectory weights, grad_waypoint_lean); the
+// host-API kernels keep the reference's element order (½·z² per element, summed).
+template <int D, bool WHOLE = false, bool POT = true, bool LEAN = false>
 __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)[D], const float (&v)[D],
                                               const float* __restrict__ ob, WP<D>& w,
                                               const f32x4* oreg = nullptr) {  // oreg: the 12-obstacle
@@ -228,7 +269,7 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
     bool big = false;
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-        cum[d] = (d ? cum[d - 1] : 0.f) + q[d];
+        cum[d] = d ? cum[d - 1] + q[d] : q[d];
         big |= fabsf(cum[d]) > 1.0e4f;
     }
     // One wave-uniform branch for all joints: the D polynomial chains share a basic block (the
@@ -253,8 +294,8 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
         py[d] = fy;
         xs[d] = -(P.link[d] * sn);
         ys[d] = P.link[d] * cs;
-        Sx += xs[d];
-        Sy += ys[d];
+        Sx = d ? Sx + xs[d] : xs[d];
+        Sy = d ? Sy + ys[d] : ys[d];
     }
     // Obstacles are staged in LDS in pairs (x_a, x_b, y_a, y_b), padded to a multiple of 4
     // with sentinels at (1e20, 1e20): r² overflows to +inf, rcp → 0, so a sentinel adds
@@ -291,8 +332,12 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
                 const f32x2 e = pkfma(dy[i], dy[i], pkfma(dx[i], dx[i], one));
                 u[i] = f32x2{__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
             }
+            // (the sums start from the first pair, not from +0: the same values, two instructions fewer)
+            cv2 = u[0];
+            ax2 = dx[0] * (u[0] * u[0]);
+            ay2 = dy[0] * (u[0] * u[0]);
 #pragma unroll
-            for (int i = 0; i < 6; ++i) {
+            for (int i = 1; i < 6; ++i) {
                 cv2 += u[i];
                 const f32x2 u2 = u[i] * u[i];
                 ax2 = pkfma(dx[i], u2, ax2);
@@ -313,8 +358,8 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
         float Cx = 0.f, Cy = 0.f;
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            Cx += xs[d];
-            Cy += ys[d];
+            Cx = d ? Cx + xs[d] : xs[d];
+            Cy = d ? Cy + ys[d] : ys[d];
             w.jx[d] = (xs[d] + Sx) - Cx;
             w.jy[d] = (ys[d] + Sy) - Cy;
         }
@@ -350,10 +395,20 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
     for (int d = 0; d < D; ++d) {
         const float z = (q[d] - P.mean_pos) * P.inv_std_pos;
         const bool m = (q[d] > P.thr_hi) || (q[d] < P.thr_lo);
-        jp += (P.cvdl && !m) ? 0.f : 0.5f * (z * z);
         const float zv = v[d] * P.inv_vmax;
         const bool mv = fabsf(v[d]) > P.thr_v;
-        jv += (P.cvdl && !mv) ? 0.f : 0.5f * (zv * zv);
+        if constexpr (LEAN) {
+            const float zm = (P.cvdl && !m) ? 0.f : z, zvm = (P.cvdl && !mv) ? 0.f : zv;
+            if constexpr (kLeanKeep<D>) {
+                w.zm[d] = zm;
+                w.zvm[d] = zvm;
+            }
+            jp = fmaf(zm, zm, jp);
+            jv = fmaf(zvm, zvm, jv);
+        } else {
+            jp += (P.cvdl && !m) ? 0.f : 0.5f * (z * z);
+            jv += (P.cvdl && !mv) ? 0.f : 0.5f * (zv * zv);
+        }
         tx = fmaxf(tx, q[d]);
         tn = fminf(tn, q[d]);
         va = fmaxf(va, fabsf(v[d]));
@@ -438,26 +493,46 @@ __device__ __forceinline__ void grad_waypoint(const KParams& P, const WP<D>& w, 
     }
 }
 
-// grad_waypoint with the start/goal rows' selection precomputed per lane (loop-invariant): epf = 1 on
-// rows 0 and N−1 (else 0), tg = the row's target (start on row 0, goal on row N−1).  The same values
-// as grad_waypoint wherever a term is non-zero (an interior row's 0·(q − tg) may be −0).
+// Per-trajectory weights of the LEAN evaluation (uniform; ljl changes with the outer iteration):
+// the loss's mean / penalty terms u = c_mean·cv + c_pen·(Σzm² + Σzvm²) (trajectory.py:85-87, 281 with
+// ½ and 1/N folded), the gradient's penalty slopes k_pos = λjl/(σ_q·N), k_vel = λjl/(v_max·N)
+// (trajectory.py:231-242, 259-268: (q − μ)/σ_q²/N = zm·(1/σ_q)/N).
+struct LeanW {
+    float c_mean, c_pen, k_pos, k_vel;
+};
+__device__ __forceinline__ LeanW lean_weights(const KParams& P, float ljl) {
+    LeanW c;
+    c.c_mean = P.one_m_lmax * P.invN;
+    c.c_pen = (0.5f * ljl) * P.invN;
+    c.k_pos = (ljl * P.inv_std_pos) * P.invN;
+    c.k_vel = (ljl * P.inv_vmax) * P.invN;
+    return c;
+}
+
+// Gradient inputs a, b of one waypoint from a LEAN evaluation (grad_waypoint's terms, the penalty
+// masks and normalised deviations reused from the evaluation).  lsg_ep = λsg on rows 0 and N−1, else
+// 0 (per lane); tg the row's start / goal.
 template <int D>
-__device__ __forceinline__ void grad_waypoint_ep(const KParams& P, const WP<D>& w, const float (&q)[D],
-                                                 const float (&v)[D], int n, int idx, float lsg, float ljl,
-                                                 float epf, const float (&tg)[D], float (&a)[D], float (&b)[D]) {
-    const float wt = (n == idx ? P.lam_max : 0.f) + P.one_m_lmax * P.invN;
+__device__ __forceinline__ void grad_waypoint_lean(const KParams& P, const WP<D>& w, const float (&q)[D],
+                                                   const float (&v)[D], bool isidx, float lsg_ep,
+                                                   const LeanW& c, const float (&tg)[D], float (&a)[D],
+                                                   float (&b)[D]) {
+    const float wt = (isidx ? P.lam_max : 0.f) + c.c_mean;
     const float wx = wt * w.gx, wy = wt * w.gy;
+    float zm[D], zvm[D];
+    if constexpr (kLeanKeep<D>) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            zm[d] = w.zm[d];
+            zvm[d] = w.zvm[d];
+        }
+    } else {
+        lean_pen<D>(P, q, v, zm, zvm);
+    }
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-        const float sgp = epf * (q[d] - tg[d]);
-        const float sgv = epf * v[d];
-        float jpg = 0.f, jvg = 0.f;
-        const bool m = (q[d] > P.thr_hi) || (q[d] < P.thr_lo);
-        if (!P.cvdl || m) jpg = ((q[d] - P.mean_pos) * P.inv_std2) * P.invN;
-        const bool mv = fabsf(v[d]) > P.thr_v;
-        if (!P.cvdl || mv) jvg = (v[d] * P.inv_vmax2) * P.invN;
-        a[d] = fmaf(ljl, jpg, fmaf(lsg, sgp, fmaf(wx, w.jx[d], wy * w.jy[d])));
-        b[d] = fmaf(lsg, sgv, ljl * jvg);
+        a[d] = fmaf(c.k_pos, zm[d], fmaf(lsg_ep, q[d] - tg[d], fmaf(wx, w.jx[d], wy * w.jy[d])));
+        b[d] = fmaf(lsg_ep, v[d], c.k_vel * zvm[d]);
     }
 }
 
@@ -733,18 +808,17 @@ __device__ __forceinline__ void ered_store(bool live, float cv, float us, float 
     s += dppf<0x141>(s);
     m = maxpos(m, dppf<0x140>(m));
     s += dppf<0x140>(s);
-    // cross-row combine with the CDNA4 row / half swaps: (r0 ∘ r1) ∘ (r2 ∘ r3) in every lane, the
-    // association of the readlane form (lanes 0, 16, 32, 48)
+    // cross-row combine with the GFX9 row broadcasts: row_bcast:15 into rows 1 and 3, row_bcast:31 into
+    // rows 2 and 3, so lane 63 holds (r3 ∘ r2) ∘ (r1 ∘ r0) — the association of the readlane form
+    // (lanes 0, 16, 32, 48), fp addition being commutative; read back as a wave-uniform value
     float wm, ws;
     {
-        auto pm = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
-        auto ps = __builtin_amdgcn_permlane16_swap(__float_as_uint(s), __float_as_uint(s), false, false);
-        const float m2 = maxpos(__uint_as_float(pm[0]), __uint_as_float(pm[1]));
-        const float s2 = __uint_as_float(ps[0]) + __uint_as_float(ps[1]);
-        auto qm = __builtin_amdgcn_permlane32_swap(__float_as_uint(m2), __float_as_uint(m2), false, false);
-        auto qs = __builtin_amdgcn_permlane32_swap(__float_as_uint(s2), __float_as_uint(s2), false, false);
-        wm = maxpos(__uint_as_float(qm[0]), __uint_as_float(qm[1]));
-        ws = __uint_as_float(qs[0]) + __uint_as_float(qs[1]);
+        m = maxpos(m, __int_as_float(__builtin_amdgcn_update_dpp((int)0x80000000, __float_as_int(m), 0x142, 0xA, 0xF, false)));
+        s = bcast_add<15>(s);
+        m = maxpos(m, __int_as_float(__builtin_amdgcn_update_dpp((int)0x80000000, __float_as_int(m), 0x143, 0xC, 0xF, false)));
+        s = bcast_add<31>(s);
+        wm = lanef(m, 63);
+        ws = lanef(s, 63);
     }
     const unsigned long long hit = __ballot(live && cv == wm);
     const int idx = hit ? n0 + __builtin_ctzll(hit) : 0x7fffffff;
@@ -1486,11 +1560,16 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
         WP<D> w;
         if (ev) {
             if (valid) {
-                if constexpr (S::kVariants) eval_waypoint_rt<D>(P, q2, v2, obs, w);
-                else eval_waypoint<D>(P, q2, v2, obs, w);
+                if constexpr (S::kVariants) {
+                    if (P.whole_robot) eval_waypoint<D, true, true, true>(P, q2, v2, obs, w);
+                    else eval_waypoint<D, false, true, true>(P, q2, v2, obs, w);
+                } else {
+                    eval_waypoint<D, false, true, true>(P, q2, v2, obs, w);
+                }
             }
             IRM_STAMP(8);
-            const float us = fmaf(P.one_m_lmax, w.cv * P.invN, ljl * ((w.jp + w.jv) * P.invN));
+            const LeanW cw = lean_weights(P, ljl);
+            const float us = fmaf(cw.c_mean, w.cv, cw.c_pen * (w.jp + w.jv));
             ered_store(valid, w.cv, us, w.tx, w.tn, w.va, phase == PH_RESYNC, n0, red, wave);
             if (valid && (n == 0 || n == N - 1)) {  // trajectory.py:183-204 rows 0 and N−1
                 float a = 0.f, bb = 0.f;
@@ -1633,9 +1712,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && !REGOPS) ? 2 : 1) void k_opti
             // ------------------------- gradient inputs at T2, mixed by JᵀJ (→ y' = y·JᵀJ)
             bool bfar = false;
             if (valid) {
-                float a[D], bb[D];
-                grad_waypoint<D>(P, w, q2, v2, n, cidx, lsg_e, ljl_e, s, g, a, bb);
+                float a[D], bb[D], tg[D];
                 const bool endrow = (n == 0 || n == N - 1);
+#pragma unroll
+                for (int k = 0; k < D; ++k) tg[k] = (n == N - 1) ? g[k] : s[k];
+                grad_waypoint_lean<D>(P, w, q2, v2, n == cidx, endrow ? lsg_e : 0.f, lean_weights(P, ljl_e), tg, a, bb);
 #pragma unroll
                 for (int k = 0; k < D; ++k) {
                     float ma = 0.f, mb = 0.f;
@@ -1878,11 +1959,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     float* obsL = smem + H.obs;
     const int nsplit = sh.NSPLIT, zsplit = lean_zsplit(sh.NSPLIT, VL);
     const LeanX LX = lean_extra(plan_lds(P, false, true, true).total, MP, NK, RP, nsplit, VL);
-    float* hL = smem + LX.hl;  // endpoint columns of F·Fᵀ (2·MP), read per round when WPL > 1
-    float* hVL = smem + LX.hv; // G's endpoint columns (2·NK), read per round when WPL > 1
     float* Eb = smem + LX.eb;  // e' rows [column][waypoint]
     float* Zp = smem + LX.zp;  // stage-1 partials of V_Rᵀ·e'
     float* Gb = smem + LX.gb;  // (V_R·y'')[waypoint] rows [column][waypoint]
+    // b'[0], b'[N−1] of this trajectory (a copy of X's endpoint velocity rows, written with them): the B
+    // operand of stage 1's endpoint MFMA (below)
+    float* EPt = smem + LX.ep + t * 2 * kEpS;
+    static_assert(D <= kEpS, "endpoint rows fit their slots");
     const float* VT = VL ? smem + LX.vt : P.VTp;
     const float* VN = VL ? smem + LX.vn : P.VNp;
 
@@ -1922,26 +2005,18 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 if (tile < MT2 && i < KQ2) a2[j * 2 + i] = g2[((size_t)tile * KQ2 + i) * 64 + lane];
             }
     }
-    // endpoint operator columns: in VGPRs for one waypoint per lane; with two (C4: 256 VGPRs) they
-    // are read from an LDS copy each round instead, which keeps the variant free of scratch spills
-    constexpr bool kHL = WPL > 1;
-    float h0T[WPL], h1T[WPL], h0V[WPL], h1V[WPL], hv0[WPL], hv1[WPL];
-#pragma unroll
-    for (int j = 0; j < WPL; ++j) {
-        h0T[j] = (vl[j] && !kHL) ? P.Hend[nn[j]] : 0.f;
-        h1T[j] = (vl[j] && !kHL) ? P.Hend[MP + nn[j]] : 0.f;
-        h0V[j] = (vl[j] && !kHL) ? P.Hend[NK + nn[j]] : 0.f;
-        h1V[j] = (vl[j] && !kHL) ? P.Hend[MP + NK + nn[j]] : 0.f;
-        hv0[j] = (vl[j] && !kHL) ? P.HV[nn[j]] : 0.f;
-        hv1[j] = (vl[j] && !kHL) ? P.HV[NK + nn[j]] : 0.f;
-    }
-    // BLS: F's endpoint velocity rows for the ‖G‖ / alpha_norm rows r = li < RP
-    const float fb0 = (BLS && tvalid && li < RP) ? P.Fbot[li] : 0.f;
-    const float fb1 = (BLS && tvalid && li < RP) ? P.Fbot[(size_t)(N - 1) * RP + li] : 0.f;
-    if constexpr (kHL) {
-        for (int e = tid; e < 2 * MP; e += P.BT) hL[e] = P.Hend[e];
-        for (int e = tid; e < 2 * NK; e += P.BT) hVL[e] = P.HV[e];
-    }
+    // The endpoint velocity rows b'[0], b'[N−1] (stage 1's operator Fᵀ has zero columns there, so that a
+    // sparse round can skip the velocity half) enter y'' through one more MFMA per stage-1 row tile, on
+    // the split-0 units: k = 0 ↔ b'[0], k = 1 ↔ b'[N−1], k = 2, 3 zero.  A = the operator's endpoint
+    // columns Fᵀ[r][NK], Fᵀ[r][NK + N − 1] (F_bot rows 0 and N − 1), held in one VGPR for the launch;
+    // B = the trajectory's compact copy of the two rows (EPt, column cl = t·D + k).  Stage 2 then sees
+    // them in y'' like every other row: the direction F·(y'' + z), G = V_R·y'' and the BLS norms need no
+    // endpoint terms of their own.
+    const bool hasep = has1 && sp1 == 0;  // wave-uniform
+    float aep = 0.f;
+    if (hasep && (lane >> 4) < 2) aep = P.Fbot[(size_t)((lane >> 4) ? N - 1 : 0) * RP + tile1 * 16 + (lane & 15)];
+    // this lane's B address: column cl of trajectory cl / D, row k = lane >> 4 (a zero slot for k ≥ 2)
+    const int epoff = (lane >> 4) < 2 ? LX.ep + (cl / D) * 2 * kEpS + (lane >> 4) * kEpS + cl % D : LX.ep0;
     if constexpr (VL) {
         const int nv = (int)frag_floats(RP, NK) / 4;  // = frag_floats(NK, RP) / 4
         const f32x4* gt = reinterpret_cast<const f32x4*>(P.VTp);
@@ -1954,6 +2029,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         }
     }
     for (int e = tid; e < 16 * lde; e += P.BT) Eb[e] = 0.f;  // no pending residual; rows ≥ N stay 0
+    for (int e = tid; e < kMaxTraj * 2 * kEpS + 4; e += P.BT) smem[LX.ep + e] = 0.f;  // + the zero word
     stage_obstacles(P, tb0, ntb, obsL);
     stage_alpha<D>(P, tb0, ntb, X, NK);
     if (tid < 2) fw[tid] = 0u;
@@ -1966,7 +2042,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         s[k] = tvalid ? P.start[b * D + k] : 0.f;
         g[k] = tvalid ? P.goal[b * D + k] : 0.f;
     }
-    float epf[WPL], tg[WPL][D];  // start/goal rows of grad_waypoint_ep, per lane
+    float epf[WPL], tg[WPL][D];  // start/goal rows of the gradient inputs, per lane
 #pragma unroll
     for (int j = 0; j < WPL; ++j) {
         epf[j] = (nn[j] == 0 || nn[j] == N - 1) ? 1.f : 0.f;
@@ -2016,18 +2092,25 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     auto evaluate = [&](const float (&q2)[WPL][D], const float (&v2)[WPL][D], bool ext, float ljl_e,
                         WP<D> (&w)[WPL]) {
         float cvs[WPL], us = 0.f, tx = -INFINITY, tn = INFINITY, va = 0.f;
+        const LeanW cw = lean_weights(P, ljl_e);
+        // every lane of an evaluating trajectory holds waypoints when N fills whole waves (only valid
+        // trajectories evaluate): the liveness selects of the reductions fold away
+        constexpr bool kAllLive = S::kNW > 0 && S::kNW == S::N;
+        bool lv[WPL];
+#pragma unroll
+        for (int j = 0; j < WPL; ++j) lv[j] = kAllLive || vl[j];
         if constexpr (WPL == 2) {  // both waypoints' obstacle terms in one pass (vl[0] = vl[1] = tvalid here)
             if (tvalid) {
-                eval_waypoint<D, false, false>(P, q2[0], v2[0], obs, w[0]);
-                eval_waypoint<D, false, false>(P, q2[1], v2[1], obs, w[1]);
+                eval_waypoint<D, false, false, true>(P, q2[0], v2[0], obs, w[0]);
+                eval_waypoint<D, false, false, true>(P, q2[1], v2[1], obs, w[1]);
                 potential_pair<D>(P, obs, w[0], w[1]);
             }
         }
 #pragma unroll
         for (int j = 0; j < WPL; ++j) {
-            if (WPL == 1 && vl[j]) eval_waypoint<D>(P, q2[j], v2[j], obs, w[j], OREG ? oreg : nullptr);  // oreg: read only when nq == 3
+            if (WPL == 1 && lv[j]) eval_waypoint<D, false, true, true>(P, q2[j], v2[j], obs, w[j], OREG ? oreg : nullptr);  // oreg: read only when nq == 3
             cvs[j] = w[j].cv;
-            const float u = fmaf(P.one_m_lmax, w[j].cv * P.invN, ljl_e * ((w[j].jp + w[j].jv) * P.invN));
+            const float u = fmaf(cw.c_mean, w[j].cv, cw.c_pen * (w[j].jp + w[j].jv));
             if (j == 0) {
                 us = u;
                 tx = w[j].tx;
@@ -2041,11 +2124,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             }
         }
         IRM_STAMP(6);
-        ered_store_wpl<WPL>(vl, cvs, us, tx, tn, va, ext, n0, NWL, red, wave);
+        ered_store_wpl<WPL>(lv, cvs, us, tx, tn, va, ext, n0, NWL, red, wave);
 #pragma unroll
         for (int j = 0; j < WPL; ++j) {
             const int n = nn[j];
-            if (vl[j] && (n == 0 || n == N - 1)) {  // trajectory.py:183-204 rows 0 and N−1
+            if (lv[j] && (n == 0 || n == N - 1)) {  // trajectory.py:183-204 rows 0 and N−1
                 float a = 0.f, bb = 0.f;
 #pragma unroll
                 for (int d = 0; d < D; ++d) {
@@ -2141,12 +2224,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     auto grad_inputs = [&](const WP<D> (&w)[WPL], const float (&q2)[WPL][D], const float (&v2)[WPL][D], int cidx,
                            float lsg_e, float ljl_e) {
         bool bfar = false;
+        const LeanW cw = lean_weights(P, ljl_e);
 #pragma unroll
         for (int j = 0; j < WPL; ++j) {
             const int n = nn[j];
             if (vl[j]) {
-                float a[D], bb[D];
-                grad_waypoint_ep<D>(P, w[j], q2[j], v2[j], n, cidx, lsg_e, ljl_e, epf[j], tg[j], a, bb);
+                float a[D], bb[D], ep[D];
+                grad_waypoint_lean<D>(P, w[j], q2[j], v2[j], n == cidx, epf[j] * lsg_e, cw, tg[j], a, bb);
                 const bool endrow = epf[j] != 0.f;
 #pragma unroll
                 for (int k = 0; k < D; ++k) {
@@ -2159,6 +2243,15 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     X[(t * D + k) * ldx + swz(n, t * D + k)] = ma;
                     X[(t * D + k) * ldx + NK + swz(n, t * D + k)] = mb;
                     bfar |= (bb[k] != 0.f) & !endrow;  // branch-free
+                    ep[k] = mb;
+                }
+                if (endrow) {  // the compact copy of the endpoint rows (read at the next round's top)
+                    if (n == 0)
+#pragma unroll
+                        for (int k = 0; k < D; ++k) EPt[k] = ep[k];
+                    if (n == N - 1)
+#pragma unroll
+                        for (int k = 0; k < D; ++k) EPt[kEpS + k] = ep[k];
                 }
             }
         }
@@ -2173,7 +2266,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // (the GD dual loop with the same prefetch: 4.33 -> 4.47 ms, 242 VGPRs there; not used)
     constexpr bool kPre1 = GD1 && FULL && kFix1;
     constexpr bool kPreW = kPre1 && RV;
-    auto stage1_load = [&](f32x4 (&bv)[KQU1], f32x4 (&bw)[KQU1]) {
+    auto stage1_load = [&](f32x4 (&bv)[KQU1], f32x4 (&bw)[KQU1], float& bep) {
         const float* xl = X + cl * ldx + r4x;
         if (has1) {  // wave-uniform
 #pragma unroll
@@ -2181,9 +2274,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 bv[i] = *reinterpret_cast<const f32x4*>(xl + (kq0 + i) * 16);
                 if constexpr (kPreW) bw[i] = *reinterpret_cast<const f32x4*>(xl + (KQa + kq0 + i) * 16);
             }
+            if (hasep) bep = smem[epoff];
         }
     };
-    auto stage1 = [&](bool full, const f32x4 (&pre)[KQU1], const f32x4 (&prew)[KQU1]) {  // Ypart[sp] = Fᵀ·[a'; b'] over this wave's unit
+    // Ypart[sp] = Fᵀ·[a'; b'] over this wave's unit (+ the endpoint rows' MFMA on the split-0 units)
+    auto stage1 = [&](bool full, const f32x4 (&pre)[KQU1], const f32x4 (&prew)[KQU1], float prep) {
         if (!has1) return;
         const float* xl = X + cl * ldx + r4x;
         constexpr bool kFix = kFix1;
@@ -2206,6 +2301,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             }
         }
         f32x4 acc0 = z4, acc1 = z4;
+        if (hasep) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(aep, kPre1 ? prep : smem[epoff], acc1, 0, 0, 0);
 #pragma unroll
         for (int i = 0; i < KQU; ++i) {
             if (in(i)) {
@@ -2342,16 +2438,18 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
             for (int g = 0; g < kGT; ++g) asm volatile("" ::"v"(ga[g][1]));
             __builtin_amdgcn_sched_barrier(0);
-            f32x4 bz = {0.f, 0.f, 0.f, 0.f};
-            f32x2 b1 = {0.f, 0.f};
-            by[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+            // the sums start from the first partial (not from +0: four adds fewer per quad; a partial
+            // of −0 stays −0, which changes no MFMA product sum that is not exactly zero)
+            f32x4 bz = zq[0];
+            f32x2 b1 = {yq[0].x, yq[0].y};
+            by[0] = yp[0];
 #pragma unroll
-            for (int sp = 0; sp < NS; ++sp) {
+            for (int sp = 1; sp < NS; ++sp) {
                 by[0] += yp[sp];
                 b1 += f32x2{yq[sp].x, yq[sp].y};
             }
 #pragma unroll
-            for (int sp = 0; sp < kZS; ++sp) bz += zq[sp];
+            for (int sp = 1; sp < kZS; ++sp) bz += zq[sp];
             bt[0] = by[0] + bz;
             by[1] = bt[1] = f32x4{b1.x, b1.y, 0.f, 0.f};
         }
@@ -2432,28 +2530,19 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4x) = ag;
         }
     };
-    // this lane's direction rows Δ = (F·y'')·J for waypoint j (endpoint velocity rows through
-    // their operator columns: stage 1's operator has zero columns there)
-    auto direction = [&](int j, const float (&e0)[D], const float (&e1)[D], float (&dt)[D], float (&dv)[D]) {
+    // this lane's direction rows Δ = (F·y'')·J for waypoint j (the endpoint velocity rows are in y'')
+    auto direction = [&](int j, float (&dt)[D], float (&dv)[D]) {
         float ut[D], uv[D];
 #pragma unroll
         for (int k = 0; k < D; ++k) {
             ut[k] = dP[(t * D + k) * ldx + swz(nn[j], t * D + k)];
             uv[k] = dP[(t * D + k) * ldx + NK + swz(nn[j], t * D + k)];
-            if constexpr (kHL) {
-                const int r = vl[j] ? nn[j] : 0;
-                ut[k] = fmaf(hL[r], e0[k], fmaf(hL[MP + r], e1[k], ut[k]));
-                uv[k] = fmaf(hL[NK + r], e0[k], fmaf(hL[MP + NK + r], e1[k], uv[k]));
-            } else {
-                ut[k] = fmaf(h0T[j], e0[k], fmaf(h1T[j], e1[k], ut[k]));
-                uv[k] = fmaf(h0V[j], e0[k], fmaf(h1V[j], e1[k], uv[k]));
-            }
         }
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-            float a = 0.f, c = 0.f;
+            float a = ut[0] * P.J[k], c = uv[0] * P.J[k];
 #pragma unroll
-            for (int l = 0; l < D; ++l) {
+            for (int l = 1; l < D; ++l) {
                 a = fmaf(ut[l], P.J[l * D + k], a);
                 c = fmaf(uv[l], P.J[l * D + k], c);
             }
@@ -2461,12 +2550,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             dv[k] = c;
         }
     };
-    // G[n] = (V_R·y'')[n] + G's endpoint velocity columns (no mix: [a'; b'] carry Jᵀ)
-    auto grad_alpha = [&](int j, const float (&e0)[D], const float (&e1)[D], float (&G)[D]) {
+    // G[n] = (V_R·y'')[n] (no mix: [a'; b'] carry Jᵀ; the endpoint velocity rows are in y'')
+    auto grad_alpha = [&](int j, float (&G)[D]) {
         const int r = vl[j] ? nn[j] : 0;
-        const float v0 = kHL ? hVL[r] : hv0[j], v1 = kHL ? hVL[NK + r] : hv1[j];
 #pragma unroll
-        for (int k = 0; k < D; ++k) G[k] = fmaf(v0, e0[k], fmaf(v1, e1[k], Gb[(t * D + k) * lde + swz(r, t * D + k)]));
+        for (int k = 0; k < D; ++k) G[k] = Gb[(t * D + k) * lde + swz(r, t * D + k)];
     };
     auto snapshot = [&](irm_stats& st) {  // extended-vis frame after a non-breaking inner iteration
         if (rec && st.series_len < P.max_series) {
@@ -2549,7 +2637,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
     for (int par = 0;; par ^= 1) {
         f32x4 pre1[KQU1], pre1w[KQU1];
-        if constexpr (kPre1) stage1_load(pre1, pre1w);
+        float pre1e = 0.f;
+        if constexpr (kPre1) stage1_load(pre1, pre1w, pre1e);
         const unsigned fl = fw[par];
         if constexpr (GD1) {
             if ((fl & 0x7FFFFFFFu) == 0u) break;  // every trajectory of the block is done
@@ -2560,25 +2649,17 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         const bool dirr = GD1 || ((fl >> 28) & 1u);  // some trajectory needs a direction this round
         const bool rsy = !GD1 && ((fl >> 29) & 1u);  // some trajectory ends an inner loop this round
         if (tid == 0) fw[par ^ 1] = 0u;
-        // the endpoint velocity rows of this trajectory's gradient inputs (their operator columns)
-        float e0[D], e1[D];
-#pragma unroll
-        for (int k = 0; k < D; ++k) {
-            const float* xc = X + (t * D + k) * ldx;
-            e0[k] = xc[NK + swz(0, t * D + k)];
-            e1[k] = xc[NK + swz(N - 1, t * D + k)];
-        }
         IRM_STAMP(0);
         if (dirr) {  // block-uniform
             IRM_COUNT(13, dense);
-            stage1(dense, pre1, pre1w);
+            stage1(dense, pre1, pre1w, pre1e);
             stage1z();
             IRM_STAMP(1);
             __syncthreads();
             IRM_STAMP(2);
             if constexpr (BLS) {
-                // ‖G‖² = ‖ŷ‖², alpha_norm·‖G‖ = Σ_r (ŷ_r·1)² with G = V_R·ŷ, ŷ = y'' + the endpoint
-                // velocity rows (optimizer_BLS.py:165-166 without forming G), rows r = li < RP of the
+                // ‖G‖² = ‖y''‖², alpha_norm·‖G‖ = Σ_r (y''_r·1)² with G = V_R·y'' (optimizer_BLS.py:165-166
+                // without forming G; the endpoint velocity rows are in y''), rows r = li < RP of the
                 // trajectory's first wave
                 if (needs_dir && n0 == 0) {  // wave-uniform
                     float g2 = 0.f, s1 = 0.f;
@@ -2586,8 +2667,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                         float sa = 0.f;
 #pragma unroll
                         for (int a = 0; a < D; ++a) {
-                            float y = fmaf(fb0, e0[a], fb1 * e1[a]);
-                            for (int sp = 0; sp < nsplit; ++sp) y += Ypart[(sp * 16 + t * D + a) * ldy + swz(li, t * D + a)];
+                            float y = Ypart[(t * D + a) * ldy + swz(li, t * D + a)];
+                            for (int sp = 1; sp < nsplit; ++sp) y += Ypart[(sp * 16 + t * D + a) * ldy + swz(li, t * D + a)];
                             g2 = fmaf(y, y, g2);
                             sa += y;
                         }
@@ -2611,8 +2692,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             if (needs_dir) {  // wave-uniform; the inner-loop head (optimizer_BLS.py:163-166)
 #pragma unroll
                 for (int j = 0; j < WPL; ++j) {
-                    direction(j, e0, e1, dTl[j], dVl[j]);  // includes the folded residual −pend/sref
-                    grad_alpha(j, e0, e1, Gl[j]);
+                    direction(j, dTl[j], dVl[j]);  // includes the folded residual −pend/sref
+                    grad_alpha(j, Gl[j]);
                 }
                 gnorm = sqrtf(wp[t * 2]);
                 anorm = wp[t * 2 + 1] / gnorm;
@@ -2681,7 +2762,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                             dv[k] = dVl[j][k];
                         }
                     } else {
-                        direction(j, e0, e1, dt, dv);
+                        direction(j, dt, dv);
                     }
 #pragma unroll
                     for (int k = 0; k < D; ++k) {
@@ -2697,6 +2778,18 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 }
             }
             IRM_STAMP(5);
+            if constexpr (GD1) {
+                // the GD single loop's waypoint state moves to the trial point unconditionally: a
+                // rejected step ends the trajectory, whose q / v are not read again (the epilogue
+                // evaluates α exactly) — no copies on the accept path
+#pragma unroll
+                for (int j = 0; j < WPL; ++j)
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        q[j][k] = q2[j][k];
+                        v[j][k] = v2[j][k];
+                    }
+            }
             // an inner loop's end is evaluated with the next outer iteration's λ (its loss and gradient
             // start that iteration; the constraint terms do not depend on λ)
             const bool rs = !GD1 && phase == LP_RESYNC;
@@ -2846,7 +2939,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
                         for (int k = 0; k < D; ++k) G[k] = Gl[j][k];
                     } else {
-                        grad_alpha(j, e0, e1, G);
+                        grad_alpha(j, G);
                     }
                     // the D element chains first (one basic block, interleaved), then the residual stores
                     float eo[D];
@@ -2859,8 +2952,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                         } else {
                             al[j][k] = alpha_step_gd(al[j][k], cj, stepj, G[k], er);
                         }
-                        q[j][k] = q2[j][k];
-                        v[j][k] = v2[j][k];
+                        if constexpr (!GD1) {
+                            q[j][k] = q2[j][k];
+                            v[j][k] = v2[j][k];
+                        }
                         if constexpr (BLS) {
                             pend[j][k] = fmaf(keep, pend[j][k], er);
                             eo[k] = nsr * pend[j][k];
