@@ -42,6 +42,8 @@ VARIANTS = {
     "prof": ("libirm_hip_prof.so", ["-DIRM_PHASE_PROFILE"]),
     # every unit with the default scheduler (tools/sched_check.py compares it bit for bit)
     "defsched": ("libirm_hip_defsched.so", ["-DIRM_DEFAULT_SCHED"]),
+    # the DynShape units with the iterative-ILP scheduler too (the D = 5 divergence check)
+    "dynilp": ("libirm_hip_dynilp.so", ["-DIRM_DYN_ILP"]),
 }
 
 
@@ -133,6 +135,8 @@ def build(force=False, verbose=False, variant="", jobs=None):
         deps = [os.path.join(CSRC, src), __file__] + HEADERS
         if oname == "irm_host":  # carries the hash of every source
             deps = deps + source_files()
+        if "-DIRM_DYN_ILP" in extra and oname.startswith("opt_dyn"):
+            flags = flags + ILP_SCHED
         if force or _newer(obj, deps):
             todo.append([HIPCC] + CFLAGS + extra + flags + ["-c", "-o", obj, os.path.join(CSRC, src)])
 

@@ -677,9 +677,13 @@ __device__ void stage_alpha(const KParams& P, int tb0, int ntb, float* X, int xr
 // U: K / dK rows per software-pipelined batch (8 in the prologue / epilogue; the optimiser loop's resync
 // rounds use 2, which keeps the register peak of the dual-loop / BLS instantiations low — spill-free —
 // at the cost of less latency hiding in a round that runs once per outer iteration)
+// Jm: J (D×D) from where the caller keeps it (default P.J) — inside the optimiser loop an LDS copy, whose
+// reads are not hoisted: the D² fp64 conversions of P.J hoisted out of the round loop held 2·D² VGPRs
 template <int D, int U = 8>
 __device__ void eval_exact(const KParams& P, const float* __restrict__ Xa, int n, float (&q)[D], float (&v)[D],
-                           const float* Kt = nullptr, const float* dKt = nullptr, int rs = kLd, int cs = 1) {
+                           const float* Kt = nullptr, const float* dKt = nullptr, int rs = kLd, int cs = 1,
+                           const float* Jm = nullptr) {
+    const float* J = Jm ? Jm : P.J;
     const int N = P.N;
     double aq[D], av[D];
 #pragma unroll
@@ -749,8 +753,62 @@ __device__ void eval_exact(const KParams& P, const float* __restrict__ Xa, int n
         double sq = 0.0, sv = 0.0;
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            sq = fma((double)tq[d], (double)P.J[d * D + k], sq);
-            sv = fma((double)tv[d], (double)P.J[d * D + k], sv);
+            sq = fma((double)tq[d], (double)J[d * D + k], sq);
+            sv = fma((double)tv[d], (double)J[d * D + k], sv);
+        }
+        q[k] = (float)sq;
+        v[k] = (float)sv;
+    }
+}
+
+// eval_exact for one lane inside the optimiser loop (the lean kernel's resyncs at D > 3): the same sums
+// in the same order, as one loop over m whose K / dK loads run PF rows ahead, J read from LDS (Jl).
+// eval_exact's batched form kept ~80 more VGPRs live around the resync at D = 7 (its fp64 J products
+// hoisted out of the round loop, and the batch's addressing): the 7-DoF dual-loop / BLS kernels spilled.
+template <int D, int PF>
+__device__ __forceinline__ void eval_exact_loop(const KParams& P, const float* __restrict__ Xc, int ldc, int n, int N,
+                                                const float* Jl, float (&q)[D], float (&v)[D]) {
+    const unsigned un = (unsigned)n, uN = (unsigned)N;
+    double aq[D], av[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) aq[d] = av[d] = 0.0;
+    float kq = P.Kt[un], kv = P.dKt[un];
+#pragma unroll 1
+    for (int m = 0; m < N; m += PF) {
+        float nq[PF], nv[PF];
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {  // rows m+1 … m+PF (clamped: the last rows re-read row N − 1)
+            const unsigned mn = (unsigned)min(m + 1 + u, N - 1);
+            nq[u] = P.Kt[mn * uN + un];
+            nv[u] = P.dKt[mn * uN + un];
+        }
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            if (PF == 1 || m + u < N) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) {
+                    const double x = (double)Xc[d * ldc + m + u];
+                    aq[d] = fma((double)kq, x, aq[d]);
+                    av[d] = fma((double)kv, x, av[d]);
+                }
+            }
+            kq = nq[u];
+            kv = nv[u];
+        }
+    }
+    float tq[D], tv[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        tq[d] = (float)aq[d];
+        tv[d] = (float)av[d];
+    }
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        double sq = 0.0, sv = 0.0;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            sq = fma((double)tq[d], (double)Jl[d * D + k], sq);
+            sv = fma((double)tv[d], (double)Jl[d * D + k], sv);
         }
         q[k] = (float)sq;
         v[k] = (float)sv;
@@ -869,6 +927,18 @@ __device__ __forceinline__ float alpha_step(float al, float c, float lr, float g
 }
 
 // alpha_step for GD (ĝ = G, step = lr): step·G is the reference's own product p2, so its term drops.
+// α' = fl(fl(c·α) − fl(lr·G)) (optimizer_GD.py:81) and the scaled residual the direction folds in,
+// e' = −(α' − (c·α − lr·G))/lr = (c·α − α')/lr − G, as u = fl(c·α − α') (one rounding, |u| ≈ |lr·G|) and
+// e' = fl(u·(1/lr) − G) (ne = −1/lr): the residual to 2^-24 of |G| (i.e. the waypoint state to 2^-24 of a
+// step per step, below the rank-16 direction's own 1.5e-7) in two FMAs instead of TwoSum and the two
+// product errors (alpha_step_gd: 9 more VALU per component on the round's critical path)
+__device__ __forceinline__ float alpha_step_gd2(float al, float c, float lr, float G, float ne, float& eo) {
+    const float p1 = unfused(c * al), p2 = unfused(lr * G);
+    const float an = unfused(p1 - p2);
+    const float u = fmaf(c, al, -an);
+    eo = fmaf(-u, ne, -G);
+    return an;
+}
 __device__ __forceinline__ float alpha_step_gd(float al, float c, float lr, float G, float& e) {
     const float p1 = unfused(c * al), p2 = unfused(lr * G);
     const float an = unfused(p1 - p2);
@@ -1944,6 +2014,12 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         nn[j] = li + j * NWL;
         vl[j] = tvalid && nn[j] < N;
     }
+    // every lane of a valid trajectory holds waypoints when N fills whole waves: wherever only valid
+    // trajectories run (evaluation, gradient inputs, the α update), the waypoint guards fold away
+    constexpr bool kAllLive = S::kNW > 0 && S::kNW == S::N;
+    bool wl[WPL];  // vl[j] where the trajectory is known to be valid
+#pragma unroll
+    for (int j = 0; j < WPL; ++j) wl[j] = kAllLive || nn[j] < N;
     const size_t b = (size_t)(tb0 + (tvalid ? t : 0));
     const bool rec = !GD1 && P.record_series && P.series;
     Prof prof;
@@ -2033,6 +2109,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     stage_obstacles(P, tb0, ntb, obsL);
     stage_alpha<D>(P, tb0, ntb, X, NK);
     if (tid < 2) fw[tid] = 0u;
+    // J for the resyncs' exact evaluations (eval_exact's Jm), in the head's parameter block
+    float* Jl = smem + H.cold + C_J;
+    if (tid < D * D) Jl[tid] = P.J[tid];
     __syncthreads();
     // the reference's α (fp32, this lane's waypoint rows) and T0 = (K·α0)·J, V0 = (dK·α0)·J
     float q[WPL][D], v[WPL][D], al[WPL][D];
@@ -2043,9 +2122,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         g[k] = tvalid ? P.goal[b * D + k] : 0.f;
     }
     float epf[WPL], tg[WPL][D];  // start/goal rows of the gradient inputs, per lane
+    unsigned long long endm[WPL];  // the wave's endpoint-row lanes
 #pragma unroll
     for (int j = 0; j < WPL; ++j) {
         epf[j] = (nn[j] == 0 || nn[j] == N - 1) ? 1.f : 0.f;
+        endm[j] = __ballot(epf[j] != 0.f);
 #pragma unroll
         for (int k = 0; k < D; ++k) tg[j][k] = (nn[j] == N - 1) ? g[k] : s[k];
     }
@@ -2095,7 +2176,6 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         const LeanW cw = lean_weights(P, ljl_e);
         // every lane of an evaluating trajectory holds waypoints when N fills whole waves (only valid
         // trajectories evaluate): the liveness selects of the reductions fold away
-        constexpr bool kAllLive = S::kNW > 0 && S::kNW == S::N;
         bool lv[WPL];
 #pragma unroll
         for (int j = 0; j < WPL; ++j) lv[j] = kAllLive || vl[j];
@@ -2213,7 +2293,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         f.b1 = sgr[3];
         const float sgpc = fmaf(0.5f, f.a0, 0.5f * f.a1);  // trajectory.py:187
         const float sgvc = fmaf(0.5f, f.b0, 0.5f * f.b1);  // trajectory.py:203
-        f.nl = fmaf(lsg_e, sgpc + sgvc, fmaf(P.lam_max, cmax, usum));
+        // the same value in every lane (LDS broadcasts): as a scalar, the loss and the step decisions
+        // built on it are wave-uniform to the compiler too (scalar branches, the loss in an SGPR)
+        f.nl = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
+                                             __builtin_bit_cast(int, fmaf(lsg_e, sgpc + sgvc, fmaf(P.lam_max, cmax, usum)))));
         f.idx = cidx;
         f.tx = tx;
         f.tn = tn;
@@ -2223,12 +2306,12 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // gradient inputs at (q2, v2), mixed by Jᵀ, into X; returns "b' non-zero away from the endpoints"
     auto grad_inputs = [&](const WP<D> (&w)[WPL], const float (&q2)[WPL][D], const float (&v2)[WPL][D], int cidx,
                            float lsg_e, float ljl_e) {
-        bool bfar = false;
+        unsigned long long bfar = 0ull;  // lanes with b' ≠ 0 (as ballots of the compares: no boolean in a VGPR)
         const LeanW cw = lean_weights(P, ljl_e);
 #pragma unroll
         for (int j = 0; j < WPL; ++j) {
             const int n = nn[j];
-            if (vl[j]) {
+            if (wl[j]) {  // (valid trajectories only)
                 float a[D], bb[D], ep[D];
                 grad_waypoint_lean<D>(P, w[j], q2[j], v2[j], n == cidx, epf[j] * lsg_e, cw, tg[j], a, bb);
                 const bool endrow = epf[j] != 0.f;
@@ -2242,7 +2325,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     }
                     X[(t * D + k) * ldx + swz(n, t * D + k)] = ma;
                     X[(t * D + k) * ldx + NK + swz(n, t * D + k)] = mb;
-                    bfar |= (bb[k] != 0.f) & !endrow;  // branch-free
+                    bfar |= __ballot(bb[k] != 0.f) & ~endm[j];
                     ep[k] = mb;
                 }
                 if (endrow) {  // the compact copy of the endpoint rows (read at the next round's top)
@@ -2255,7 +2338,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 }
             }
         }
-        return __ballot(bfar) != 0ull;
+        return bfar != 0ull;
     };
     // GD single loop, fixed-shape launches: stage 1's B operand (both halves; the velocity half is used
     // in dense rounds only) is read at the top of the round, before the flag word (X was written before
@@ -2274,7 +2357,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 bv[i] = *reinterpret_cast<const f32x4*>(xl + (kq0 + i) * 16);
                 if constexpr (kPreW) bw[i] = *reinterpret_cast<const f32x4*>(xl + (KQa + kq0 + i) * 16);
             }
-            if (hasep) bep = smem[epoff];
+            bep = smem[epoff];  // (a valid word on every stage-1 wave; used on the endpoint waves)
         }
     };
     // Ypart[sp] = Fᵀ·[a'; b'] over this wave's unit (+ the endpoint rows' MFMA on the split-0 units)
@@ -2301,12 +2384,23 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             }
         }
         f32x4 acc0 = z4, acc1 = z4;
-        if (hasep) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(aep, kPre1 ? prep : smem[epoff], acc1, 0, 0, 0);
+        // fixed shapes: the second chain's first product is the endpoint MFMA's successor or starts from
+        // zero itself (one MFMA result either way: no zeroed accumulator on the non-endpoint waves)
+        if constexpr (kFix) {
+            if (hasep) {
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(aep, kPre1 ? prep : smem[epoff], z4, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[0][1], bv[0][1], acc1, 0, 0, 0);
+            } else {
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[0][1], bv[0][1], z4, 0, 0, 0);
+            }
+        } else if (hasep) {
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(aep, kPre1 ? prep : smem[epoff], acc1, 0, 0, 0);
+        }
 #pragma unroll
         for (int i = 0; i < KQU; ++i) {
             if (in(i)) {
                 acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][0], bv[i][0], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][1], bv[i][1], acc1, 0, 0, 0);
+                if (!kFix || i > 0) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][1], bv[i][1], acc1, 0, 0, 0);
                 acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][2], bv[i][2], acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[i][3], bv[i][3], acc1, 0, 0, 0);
             }
@@ -2431,7 +2525,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 yq[sp] = *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + cl) * ldy + 16 + r4x);
             }
 #pragma unroll
-            for (int sp = 0; sp < kZS; ++sp) zq[sp] = *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + r4x);
+            for (int sp = 0; sp < (BLS ? 0 : kZS); ++sp) zq[sp] = *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + r4x);
             // every quad stays whole (no narrowing, no register reuse of its unused half while in flight)
 #pragma unroll
             for (int sp = 0; sp < NS; ++sp) asm volatile("" ::"v"(yq[sp]));
@@ -2440,7 +2534,6 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             __builtin_amdgcn_sched_barrier(0);
             // the sums start from the first partial (not from +0: four adds fewer per quad; a partial
             // of −0 stays −0, which changes no MFMA product sum that is not exactly zero)
-            f32x4 bz = zq[0];
             f32x2 b1 = {yq[0].x, yq[0].y};
             by[0] = yp[0];
 #pragma unroll
@@ -2448,9 +2541,14 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 by[0] += yp[sp];
                 b1 += f32x2{yq[sp].x, yq[sp].y};
             }
+            if constexpr (BLS) {  // the BLS direction carries no residual (the trials are evaluated exactly)
+                bt[0] = by[0];
+            } else {
+                f32x4 bz = zq[0];
 #pragma unroll
-            for (int sp = 1; sp < kZS; ++sp) bz += zq[sp];
-            bt[0] = by[0] + bz;
+                for (int sp = 1; sp < kZS; ++sp) bz += zq[sp];
+                bt[0] = by[0] + bz;
+            }
             by[1] = bt[1] = f32x4{b1.x, b1.y, 0.f, 0.f};
         }
 #pragma unroll
@@ -2460,7 +2558,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 f32x4 bz = {0.f, 0.f, 0.f, 0.f};
                 for (int sp = 0; sp < nsplit; ++sp)
                     by[i] += *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + cl) * ldy + i * 16 + r4x);
-                if (i == 0) {  // z has rank 16: rows 0-15 only
+                if (i == 0 && !BLS) {  // z has rank 16: rows 0-15 only (BLS: no residual in the direction)
                     for (int sp = 0; sp < zsplit; ++sp)
                         bz += *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + r4x);
                 }
@@ -2530,6 +2628,22 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4x) = ag;
         }
     };
+    // BLS trials: dP = F·z, z = V_Rᵀ·e (the trial iterate's rounding residual e, stage1z), the F tiles at
+    // rank 16 as in stage 2 — the waypoint image L·e of the residual (F·V_Rᵀ ≈ L on the rank-16 subspace,
+    // the rest below 1e-7 of |L·e|, see stage1z)
+    auto stage2z = [&]() {
+        f32x4 bz = *reinterpret_cast<const f32x4*>(Zp + cl * ldy + r4x);
+        for (int sp = 1; sp < zsplit; ++sp) bz += *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + r4x);
+#pragma unroll
+        for (int j = 0; j < S2T; ++j) {
+            if (wave + j * nwaves < MT2) {
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2][m], bz[m], acc, 0, 0, 0);
+                *reinterpret_cast<f32x4*>(dP + cl * ldx + (wave + j * nwaves) * 16 + r4x) = acc;
+            }
+        }
+    };
     // this lane's direction rows Δ = (F·y'')·J for waypoint j (the endpoint velocity rows are in y'')
     auto direction = [&](int j, float (&dt)[D], float (&dv)[D]) {
         float ut[D], uv[D];
@@ -2552,7 +2666,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     };
     // G[n] = (V_R·y'')[n] (no mix: [a'; b'] carry Jᵀ; the endpoint velocity rows are in y'')
     auto grad_alpha = [&](int j, float (&G)[D]) {
-        const int r = vl[j] ? nn[j] : 0;
+        const int r = wl[j] ? nn[j] : 0;  // (valid trajectories only)
 #pragma unroll
         for (int k = 0; k < D; ++k) G[k] = Gb[(t * D + k) * lde + swz(r, t * D + k)];
     };
@@ -2604,7 +2718,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         } else {
             if (lane == 0 && tvalid)
                 atomicOr(&fw[0], (1u << wave) | (needs_dir ? 1u << 28 : 0u) | (phase == LP_RESYNC ? 1u << 29 : 0u) |
-                                     (bfar ? 1u << 31 : 0u));
+                                     (phase == LP_STEP ? 1u << 30 : 0u) | (bfar ? 1u << 31 : 0u));
         }
     }
     __syncthreads();
@@ -2621,23 +2735,17 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #endif
     // ---------------------------------------------------------- rounds
     float dTl[BLS ? WPL : 1][D], dVl[BLS ? WPL : 1][D], Gl[BLS ? WPL : 1][D];  // BLS: latched direction
-    // BLS: the rounding residual not yet in [T; V] (α units) and the reference step it is folded into
-    // y'' with (e' = −pend/sref): trial j applies the fraction s_j/sref of it, the rest carries over
-    // (sref ≥ kMinRefStep: after a long run of rejected trials lr/‖G‖ can fall below 1e-38, where
-    // −pend/sref would overflow to ±inf and 0·inf = NaN; a clamped sref folds the residual with a
-    // finite scale and the trials apply their fraction s_j/sref ≪ 1 of it, the rest stays pending)
-    float pend[BLS ? WPL : 1][D], sref = 1.f;
 #pragma unroll
     for (int j = 0; j < (BLS ? WPL : 1); ++j)
 #pragma unroll
-        for (int k = 0; k < D; ++k) dTl[j][k] = dVl[j][k] = Gl[j][k] = pend[j][k] = 0.f;
+        for (int k = 0; k < D; ++k) dTl[j][k] = dVl[j][k] = Gl[j][k] = 0.f;
     // The second half of the waves (4-7: the younger partner on each SIMD) loses VALU arbitration to
     // the older one in every phase; static priority for that half (MI355X_MICROARCH.md, two waves per
     // SIMD, item 4): C3 +1.7 %.  Priority only reorders issue: results are unchanged.
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
     for (int par = 0;; par ^= 1) {
         f32x4 pre1[KQU1], pre1w[KQU1];
-        float pre1e = 0.f;
+        float pre1e;  // read only on the endpoint waves (hasep)
         if constexpr (kPre1) stage1_load(pre1, pre1w, pre1e);
         const unsigned fl = fw[par];
         if constexpr (GD1) {
@@ -2653,7 +2761,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         if (dirr) {  // block-uniform
             IRM_COUNT(13, dense);
             stage1(dense, pre1, pre1w, pre1e);
-            stage1z();
+            if constexpr (!BLS) stage1z();  // (BLS: the trials' residuals have their own stage below)
             IRM_STAMP(1);
             __syncthreads();
             IRM_STAMP(2);
@@ -2692,7 +2800,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             if (needs_dir) {  // wave-uniform; the inner-loop head (optimizer_BLS.py:163-166)
 #pragma unroll
                 for (int j = 0; j < WPL; ++j) {
-                    direction(j, dTl[j], dVl[j]);  // includes the folded residual −pend/sref
+                    direction(j, dTl[j], dVl[j]);  // (F·y'')·J = L·G·J
                     grad_alpha(j, Gl[j]);
                 }
                 gnorm = sqrtf(wp[t * 2]);
@@ -2701,6 +2809,45 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 st.cost_evals++;
                 trial = 0;
                 needs_dir = false;
+            }
+        }
+        // this round's step (BLS: the trial's)
+        float cj = cfac, stepj = lr;
+        const float lrj = lr;
+        if constexpr (BLS) {
+            cj = unfused(1.f - unfused(P.lreg * lr));  // (1 − λ_reg·bls_lr) in fp32 (optimizer_BLS.py:139)
+            stepj = lr / gnorm;
+        }
+        // ------------------------------------------------ BLS: the trial's fp32 iterate and its trajectory
+        // The reference evaluates each trial at its own fp32 iterate α_j = fl(fl(c_j·α) − fl(lr_j·ĝ))
+        // (optimizer_BLS.py:139-140).  [T; V] = L·α·J holds at the start of every trial (an accepted trial
+        // brings its exact trajectory along), so L·α_j·J = c_j·[T; V] − s_j·(L·G·J) + L·e_j·J with the
+        // iterate's rounding residual e_j = α_j − (c_j·α − s_j·G) (alpha_step, error-free): e_j goes
+        // through z = V_Rᵀ·e_j and F·z (rank 16) before the evaluation, so the trial is evaluated at α_j's
+        // own trajectory to fp32 resolution — not one rounding residual behind it.
+        float aj[BLS ? WPL : 1][D];
+        if constexpr (BLS) {
+            if ((fl >> 30) & 1u) {  // block-uniform: some trajectory has a line-search trial this round
+                if (phase == LP_STEP) {  // wave-uniform
+#pragma unroll
+                    for (int j = 0; j < WPL; ++j) {
+                        float er[D];
+#pragma unroll
+                        for (int k = 0; k < D; ++k) {
+                            const float gh = Gl[j][k] / gnorm;  // n_alpha_grad (optimizer_BLS.py:165)
+                            aj[j][k] = alpha_step(al[j][k], cj, lrj, gh, stepj, Gl[j][k], er[k]);
+                        }
+                        if (vl[j]) {
+#pragma unroll
+                            for (int k = 0; k < D; ++k) Eb[(t * D + k) * lde + swz(nn[j], t * D + k)] = er[k];
+                        }
+                    }
+                }
+                __syncthreads();
+                stage1z();
+                __syncthreads();
+                stage2z();
+                __syncthreads();
             }
         }
         // ------------------------------------------------ end of an inner loop: α's exact trajectory
@@ -2713,12 +2860,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
                         for (int k = 0; k < D; ++k) {
                             X[(t * D + k) * ldx + nn[j]] = al[j][k];
-                            Eb[(t * D + k) * lde + swz(nn[j], t * D + k)] = 0.f;  // absorbed by the exact trajectory
+                            if constexpr (!BLS) Eb[(t * D + k) * lde + swz(nn[j], t * D + k)] = 0.f;  // absorbed by the exact trajectory
                         }
-                    }
-                    if constexpr (BLS) {
-#pragma unroll
-                        for (int k = 0; k < D; ++k) pend[j][k] = 0.f;
                     }
                 }
             }
@@ -2727,7 +2870,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
                 for (int j = 0; j < WPL; ++j) {
                     if (vl[j]) {
-                        eval_exact<D, kResyncU>(P, X + (t * D) * ldx, nn[j], q[j], v[j], nullptr, nullptr, 1, ldx);
+                        if constexpr (D <= 3) eval_exact<D, kResyncU>(P, X + (t * D) * ldx, nn[j], q[j], v[j], nullptr, nullptr, 1, ldx, Jl);
+                        else eval_exact_loop<D, 4>(P, X + (t * D) * ldx, ldx, nn[j], N, Jl, q[j], v[j]);
                         // the last extended-vis frame shows the exact trajectory of the returned α
                         if (rec && st.series_len > 0) {
 #pragma unroll
@@ -2741,12 +2885,6 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         }
         // ------------------------------------------------ update + evaluate
         float q2[WPL][D], v2[WPL][D];
-        float cj = cfac, stepj = lr;  // this round's step (BLS: the trial's)
-        const float lrj = lr;
-        if constexpr (BLS) {
-            cj = unfused(1.f - unfused(P.lreg * lr));  // (1 − λ_reg·bls_lr) in fp32 (optimizer_BLS.py:139)
-            stepj = lr / gnorm;
-        }
         WP<D> w[WPL];
         const bool stepping = GD1 ? !done : phase == LP_STEP;  // wave-uniform
         const bool ev = GD1 ? !done : phase != LP_DONE;
@@ -2756,18 +2894,24 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 if (stepping) {
                     float dt[D], dv[D];
                     if constexpr (BLS) {
+                        float ct[D], cv[D];
+                        direction(j, ct, cv);  // (F·z)·J = L·e_j·J, the trial iterate's rounding residual
 #pragma unroll
                         for (int k = 0; k < D; ++k) {
-                            dt[k] = dTl[j][k];
-                            dv[k] = dVl[j][k];
+                            q2[j][k] = fmaf(cj, q[j][k], -(stepj * dTl[j][k])) + ct[k];
+                            v2[j][k] = fmaf(cj, v[j][k], -(stepj * dVl[j][k])) + cv[k];
                         }
                     } else {
                         direction(j, dt, dv);
-                    }
 #pragma unroll
-                    for (int k = 0; k < D; ++k) {
-                        q2[j][k] = fmaf(cj, q[j][k], -(stepj * dt[k]));
-                        v2[j][k] = fmaf(cj, v[j][k], -(stepj * dv[k]));
+                        for (int k = 0; k < D; ++k) {
+                            const float tq = -(stepj * dt[k]), tv = -(stepj * dv[k]);
+                            q2[j][k] = fmaf(cj, q[j][k], tq);
+                            v2[j][k] = fmaf(cj, v[j][k], tv);
+                            // the products stay live past the FMAs: three-address FMAs, whose results
+                            // can take the waypoint state's own registers (no copies at the round's end)
+                            if constexpr (GD1) asm volatile("" ::"v"(tq), "v"(tv), "v"(q2[j][k]), "v"(v2[j][k]));
+                        }
                     }
                 } else {
 #pragma unroll
@@ -2908,62 +3052,41 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                         } else if (rejected_all) {
                             needs_dir = true;  // the same α: X still holds its gradient inputs
                             bfar = xdense;
-                            sref = fmaxf(lr / gnorm, kMinRefStep);  // refold the pending residual for the next trial series
-#pragma unroll
-                            for (int j = 0; j < WPL; ++j)
-                                if (vl[j])
-#pragma unroll
-                                    for (int k = 0; k < D; ++k) Eb[(t * D + k) * lde + swz(nn[j], t * D + k)] = -pend[j][k] / sref;
                         } else {
                             more = true;
                         }
                     }
                 }
             }
-            if (accept) {
-                // α' = fl(fl(c·α) − fl(lr·ĝ)) (optimizer_GD.py:81, optimizer_BLS.py:139) and its residual
-                // for the next direction (GD: −e/lr folded into stage 2's y''; BLS: e, through dC)
+            if (accept && BLS) {
+                // the trial's iterate α_j and its exact trajectory (optimizer_BLS.py:149)
+#pragma unroll
+                for (int j = 0; j < WPL; ++j)
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        al[j][k] = aj[j][k];
+                        q[j][k] = q2[j][k];
+                        v[j][k] = v2[j][k];
+                    }
+            } else if (accept) {
+                // α' = fl(fl(c·α) − fl(lr·G)) (optimizer_GD.py:81) and its residual for the next direction
+                // (−e/lr folded into stage 2's y'')
                 const float ne = GD1 ? nilr : -1.f / fmaxf(stepj, kMinRefStep);
-                // BLS: [T; V] took the fraction s_j/sref of the pending residual; the rest (scaled by
-                // c_j like α) stays pending with this trial's residual, refolded for the next direction
-                float keep = 0.f, nsr = 0.f;
-                if constexpr (BLS) {
-                    keep = cj - stepj / sref;
-                    sref = fmaxf(lr / gnorm, kMinRefStep);  // the next trial 0's step (lr already ·β+): keep ≈ 0 there
-                    nsr = -1.f / sref;
-                }
 #pragma unroll
                 for (int j = 0; j < WPL; ++j) {
                     float G[D];
-                    if constexpr (BLS) {
-#pragma unroll
-                        for (int k = 0; k < D; ++k) G[k] = Gl[j][k];
-                    } else {
-                        grad_alpha(j, G);
-                    }
+                    grad_alpha(j, G);
                     // the D element chains first (one basic block, interleaved), then the residual stores
                     float eo[D];
 #pragma unroll
                     for (int k = 0; k < D; ++k) {
-                        float er;
-                        if constexpr (BLS) {
-                            const float gh = G[k] / gnorm;  // n_alpha_grad (optimizer_BLS.py:165)
-                            al[j][k] = alpha_step(al[j][k], cj, lrj, gh, stepj, G[k], er);
-                        } else {
-                            al[j][k] = alpha_step_gd(al[j][k], cj, stepj, G[k], er);
-                        }
+                        al[j][k] = alpha_step_gd2(al[j][k], cj, stepj, G[k], ne, eo[k]);
                         if constexpr (!GD1) {
                             q[j][k] = q2[j][k];
                             v[j][k] = v2[j][k];
                         }
-                        if constexpr (BLS) {
-                            pend[j][k] = fmaf(keep, pend[j][k], er);
-                            eo[k] = nsr * pend[j][k];
-                        } else {
-                            eo[k] = er * ne;
-                        }
                     }
-                    if (vl[j]) {
+                    if (wl[j]) {
 #pragma unroll
                         for (int k = 0; k < D; ++k) Eb[(t * D + k) * lde + swz(nn[j], t * D + k)] = eo[k];
                     }
@@ -2986,7 +3109,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 }
                 if (lane == 0 && phase != LP_DONE)
                     atomicOr(&fw[par ^ 1], (1u << wave) | (needs_dir ? 1u << 28 : 0u) |
-                                               (phase == LP_RESYNC ? 1u << 29 : 0u) | (bfar ? 1u << 31 : 0u));
+                                               (phase == LP_RESYNC ? 1u << 29 : 0u) | (phase == LP_STEP ? 1u << 30 : 0u) |
+                                               (bfar ? 1u << 31 : 0u));
             }
         }
         IRM_STAMP(11);
