@@ -818,6 +818,10 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
         if (!lean_rank_cut_ok(c->lam16, c->lam24)) kp.lean_ok = 0;
         const char* w = getenv("IRM_LEAN_WPL");
         kp.lean_wpl = w ? atoi(w) : 0;
+        const char* nh = getenv("IRM_LEAN_NOHELP");
+        kp.lean_nohelp = (nh && nh[0] == '1') ? 1 : 0;
+        const char* tp = getenv("IRM_TRACE_PROBLEM");
+        kp.trace_b = tp ? atoi(tp) : 0;
     }
     c->max_series = p->max_series > 0 ? p->max_series : 1 + p->max_outer_iteration * p->max_inner_iteration;
     kp.max_series = c->max_series;

@@ -43,6 +43,8 @@ struct KParams {
     int32_t optimizer, max_inner, max_outer, max_bls, cvdl, record_series, max_series;
     int32_t lean_ok;  // k_gd_single may serve GD single-loop launches (IRM_GENERAL_KERNEL=1 clears it)
     int32_t lean_wpl; // diagnostics: IRM_LEAN_WPL=2 forces two waypoints per lane at N ≤ 128
+    int32_t lean_nohelp;  // diagnostics: IRM_LEAN_NOHELP=1 turns k_lean's BLS line-search helpers off
+    int32_t trace_b;      // diagnostics: the batch index whose line search is logged (IRM_TRACE_PROBLEM, default 0)
     float llr, lci, lsg0, ljl0, eps_p, eps_v, lmax, lreg;
     float bls_lr0, bls_a, bls_bp, bls_bm, vmax, pmax, pmin, pad1;
     // derived fp32 constants (reference casts its Python doubles to fp32)
@@ -233,12 +235,16 @@ __host__ __device__ inline Plan plan_lds(const KParams& p, bool ops_lds, bool op
 // the stage-1 splits where the LDS allows (vlds shapes: N ≤ 128, D ≤ 3), so the units stay one per wave
 __host__ __device__ constexpr int lean_zsplit(int nsplit, bool vlds) { return vlds ? 2 * nsplit : nsplit; }
 struct LeanX {
-    int vt, vn, eb, zp, gb, ep, ep0, total;
+    int vt, vn, eb, zp, gb, ep, ep0, ss, hp, total;
 };
 // compact copy of each trajectory's endpoint velocity rows b'[0], b'[N−1] of X (k_lean): kEpS floats each
 constexpr int kEpS = 8;
 __host__ __device__ constexpr int lean_ld(int NK) { return NK + 8; }
-__host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, int nsplit, bool vlds) {
+// help_threads > 0: the BLS line-search helpers' exchange regions (k_lean, kHelp): a trajectory's α, T, V
+// rows by thread ([3·D][threads], ss) and its per-round scalars (8 words per trajectory slot, hp)
+constexpr int kHpW = 8;
+__host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, int nsplit, bool vlds, int D = 0,
+                                            int help_threads = 0) {
     LeanX e{};
     int off = base;
     e.vt = e.vn = 0;
@@ -258,6 +264,13 @@ __host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, in
     off += kMaxTraj * 2 * kEpS;
     e.ep0 = off;  // one zero word (the endpoint MFMA's B for k = 2, 3)
     off += 4;
+    e.ss = e.hp = 0;
+    if (help_threads > 0) {
+        e.ss = off;
+        off += al4(3 * D * help_threads);
+        e.hp = off;
+        off += kMaxTraj * kHpW;
+    }
     e.total = off;
     return e;
 }

@@ -1970,6 +1970,13 @@ enum LeanFlow : int { LF_GD1 = 0, LF_GD2 = 1, LF_BLS = 2 };
 // Per-trajectory phase (LF_GD2 / LF_BLS): a GD step or BLS trial this round, the end of an inner
 // loop (α's exact trajectory, constraintsFulfilled, λ escalation), done.
 enum LeanPhase : int { LP_STEP = 0, LP_RESYNC = 1, LP_DONE = 2 };
+// BLS line-search helpers (k_lean): when one trajectory of a workgroup is left, the first done slot
+// evaluates its next trial (lr·β₋) in the same round.  D ≤ 3, one waypoint per lane, N ≤ 128 in
+// 512-thread workgroups (or N ≤ 64): where the exchange regions fit the LDS at full occupancy.
+template <class S, int MAXT, int WPL, bool FULL, int FLOW>
+constexpr bool lean_help() {
+    return FLOW == LF_BLS && S::D <= 3 && WPL == 1 && FULL && S::kNW > 0 && (S::NK <= 64 || (S::NK <= 128 && MAXT > 256));
+}
 
 // FULL: the launch has exactly MAXT threads, so the stage-2 tiles per wave are known exactly
 // (otherwise kS2T(MAXT) bounds them for smaller launches): C7's 256-thread variant then holds 4
@@ -2034,7 +2041,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     unsigned* fw = reinterpret_cast<unsigned*>(smem + H.flags);
     float* obsL = smem + H.obs;
     const int nsplit = sh.NSPLIT, zsplit = lean_zsplit(sh.NSPLIT, VL);
-    const LeanX LX = lean_extra(plan_lds(P, false, true, true).total, MP, NK, RP, nsplit, VL);
+    constexpr bool kHelp = lean_help<S, MAXT, WPL, FULL, FLOW>();
+    const LeanX LX = lean_extra(plan_lds(P, false, true, true).total, MP, NK, RP, nsplit, VL, D, kHelp ? MAXT : 0);
     float* Eb = smem + LX.eb;  // e' rows [column][waypoint]
     float* Zp = smem + LX.zp;  // stage-1 partials of V_Rᵀ·e'
     float* Gb = smem + LX.gb;  // (V_R·y'')[waypoint] rows [column][waypoint]
@@ -2054,13 +2062,15 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // banks) are then both conflict-free; per-row accesses stay so (a column's rows only permute).
     const int r4x = r4 ^ (cl & 4);
     auto swz = [](int r, int c) { return r ^ (c & 4); };
+    int ycl = cl;     // stage 2's Ypart column for this lane's B column (a helper round: the helper's read t*'s)
+    int r4y = r4x;    // its first row under the row swizzle of column ycl
     const bool has1 = wave < MT1 * nsplit;
     const int tile1 = wave % MT1, sp1 = wave / MT1;
     const int kq0 = (KQa * sp1) / nsplit, kq1 = (KQa * (sp1 + 1)) / nsplit;
 
     // ----------------------------------------------------------- prologue
     f32x4 a1[S1Q], a1v[RV ? S1Q : 1], a2[S2T * 2];
-    {
+    auto load_ops = [&]() {
         const f32x4* g1 = reinterpret_cast<const f32x4*>(P.F1p);
         const f32x4* g2 = reinterpret_cast<const f32x4*>(P.F2p);
 #pragma unroll
@@ -2080,7 +2090,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 const int tile = wave + j * nwaves;
                 if (tile < MT2 && i < KQ2) a2[j * 2 + i] = g2[((size_t)tile * KQ2 + i) * 64 + lane];
             }
-    }
+    };
+    load_ops();
     // The endpoint velocity rows b'[0], b'[N−1] (stage 1's operator Fᵀ has zero columns there, so that a
     // sparse round can skip the velocity half) enter y'' through one more MFMA per stage-1 row tile, on
     // the split-0 units: k = 0 ↔ b'[0], k = 1 ↔ b'[N−1], k = 2, 3 zero.  A = the operator's endpoint
@@ -2147,7 +2158,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     }
     __syncthreads();
     for (int e = tid; e < MP * kLd; e += P.BT) X[e] = 0.f;
-    const float* obs = obsL + (P.obs_stride ? t * obs_pitch(P.O) : 0);
+    const float* obs = obsL + (P.obs_stride ? t * obs_pitch(P.O) : 0);  // (a helper round: t*'s)
     // 9-12 obstacles (the reference's 11): the padded table in VGPRs for the whole launch (24 floats),
     // so the per-round evaluation does not wait on its LDS reads
 #ifndef IRM_X_OREG_ALL
@@ -2233,14 +2244,14 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // wave record per trajectory, measured 2 % slower with it; C5 / C7 1.5-2 % faster)
     constexpr bool kLatF = S::kNW > 0 && WPL == 1;
     constexpr bool kLatS = S::kNW > 0 && S::NK <= 128;   // stage 2's and the z unit's: N <= 128
-    auto finalize = [&](float lsg_e) {
+    auto finalize = [&](float lsg_e, int ft) {  // ft: the trajectory slot whose records are read
         if constexpr (!kLatF) {
-            const float* r0 = red + (t * WPTL) * 8;
+            const float* r0 = red + (ft * WPTL) * 8;
             float cmax = r0[0];
             int cidx = __float_as_int(r0[1]);
             float usum = r0[2], tx = r0[3], tn = r0[4], va = r0[5];
             for (int ww = 1; ww < WPTL; ++ww) {
-                const float* rw = red + (t * WPTL + ww) * 8;
+                const float* rw = red + (ft * WPTL + ww) * 8;
                 amax_step(cmax, cidx, rw[0], __float_as_int(rw[1]));
                 usum += rw[2];
                 tx = fmaxf(tx, rw[3]);
@@ -2248,10 +2259,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 va = fmaxf(va, rw[5]);
             }
             Fin f;
-            f.a0 = sg[t * 4 + 0];
-            f.b0 = sg[t * 4 + 1];
-            f.a1 = sg[t * 4 + 2];
-            f.b1 = sg[t * 4 + 3];
+            f.a0 = sg[ft * 4 + 0];
+            f.b0 = sg[ft * 4 + 1];
+            f.a1 = sg[ft * 4 + 2];
+            f.b1 = sg[ft * 4 + 3];
             const float sgpc = fmaf(0.5f, f.a0, 0.5f * f.a1);  // trajectory.py:187
             const float sgvc = fmaf(0.5f, f.b0, 0.5f * f.b1);  // trajectory.py:203
             f.nl = fmaf(lsg_e, sgpc + sgvc, fmaf(P.lam_max, cmax, usum));
@@ -2267,9 +2278,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
         for (int ww = 0; ww < WPTL; ++ww)
 #pragma unroll
-            for (int e = 0; e < 6; ++e) rr[ww][e] = red[(t * WPTL + ww) * 8 + e];
+            for (int e = 0; e < 6; ++e) rr[ww][e] = red[(ft * WPTL + ww) * 8 + e];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) sgr[e] = sg[t * 4 + e];
+        for (int e = 0; e < 4; ++e) sgr[e] = sg[ft * 4 + e];
         __builtin_amdgcn_sched_barrier(0);
         float cmax = rr[0][0];
         int cidx = __float_as_int(rr[0][1]);
@@ -2305,7 +2316,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     };
     // gradient inputs at (q2, v2), mixed by Jᵀ, into X; returns "b' non-zero away from the endpoints"
     auto grad_inputs = [&](const WP<D> (&w)[WPL], const float (&q2)[WPL][D], const float (&v2)[WPL][D], int cidx,
-                           float lsg_e, float ljl_e) {
+                           float lsg_e, float ljl_e, int gt) {  // gt: the trajectory slot whose X columns are written
+        float* EPg = EPt + (gt - t) * 2 * kEpS;
         unsigned long long bfar = 0ull;  // lanes with b' ≠ 0 (as ballots of the compares: no boolean in a VGPR)
         const LeanW cw = lean_weights(P, ljl_e);
 #pragma unroll
@@ -2323,18 +2335,18 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                         ma = fmaf(a[d], P.J[k * D + d], ma);
                         mb = fmaf(bb[d], P.J[k * D + d], mb);
                     }
-                    X[(t * D + k) * ldx + swz(n, t * D + k)] = ma;
-                    X[(t * D + k) * ldx + NK + swz(n, t * D + k)] = mb;
+                    X[(gt * D + k) * ldx + swz(n, gt * D + k)] = ma;
+                    X[(gt * D + k) * ldx + NK + swz(n, gt * D + k)] = mb;
                     bfar |= __ballot(bb[k] != 0.f) & ~endm[j];
                     ep[k] = mb;
                 }
                 if (endrow) {  // the compact copy of the endpoint rows (read at the next round's top)
                     if (n == 0)
 #pragma unroll
-                        for (int k = 0; k < D; ++k) EPt[k] = ep[k];
+                        for (int k = 0; k < D; ++k) EPg[k] = ep[k];
                     if (n == N - 1)
 #pragma unroll
-                        for (int k = 0; k < D; ++k) EPt[kEpS + k] = ep[k];
+                        for (int k = 0; k < D; ++k) EPg[kEpS + k] = ep[k];
                 }
             }
         }
@@ -2492,12 +2504,16 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     constexpr int kMTG = S::NK / 16, kGT = (kMTG + MAXT / 64 - 1) / (MAXT / 64);
     constexpr bool kS2Fix = FULL && S::kNW > 0;
     constexpr bool kS2Batch = kS2Fix && kLatS;  // stage 2's partial sums read in one batch
-    auto stage2 = [&]() {
+    // WF: the F tiles (dP, with the residual z folded in), WG: the G tiles (Gb).  The GD flows run both in
+    // one pass; the BLS flow runs G in the rounds with a new gradient input and F in every trial round
+    // (its trial's own residual folded in, so the direction is the trial iterate's)
+    auto stage2f = [&](auto WFc, auto WGc) {
+        constexpr bool WF = decltype(WFc)::value, WG = decltype(WGc)::value;
         f32x4 acc[S2T];
 #pragma unroll
         for (int j = 0; j < S2T; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
         f32x4 ga[kS2Fix ? kGT : 1][2];
-        if constexpr (kS2Fix) {
+        if constexpr (kS2Fix && WG) {
 #pragma unroll
             for (int g = 0; g < kGT; ++g) {
                 const int u = nwaves - 1 - wave + g * nwaves;
@@ -2521,16 +2537,16 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             f32x4 yp[NS], zq[kZS], yq[NS];
 #pragma unroll
             for (int sp = 0; sp < NS; ++sp) {
-                yp[sp] = *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + cl) * ldy + r4x);
-                yq[sp] = *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + cl) * ldy + 16 + r4x);
+                yp[sp] = *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + ycl) * ldy + r4y);
+                yq[sp] = *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + ycl) * ldy + 16 + r4y);
             }
 #pragma unroll
-            for (int sp = 0; sp < (BLS ? 0 : kZS); ++sp) zq[sp] = *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + r4x);
+            for (int sp = 0; sp < (WF ? kZS : 0); ++sp) zq[sp] = *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + r4x);
             // every quad stays whole (no narrowing, no register reuse of its unused half while in flight)
 #pragma unroll
             for (int sp = 0; sp < NS; ++sp) asm volatile("" ::"v"(yq[sp]));
 #pragma unroll
-            for (int g = 0; g < kGT; ++g) asm volatile("" ::"v"(ga[g][1]));
+            for (int g = 0; g < (WG ? kGT : 0); ++g) asm volatile("" ::"v"(ga[g][1]));
             __builtin_amdgcn_sched_barrier(0);
             // the sums start from the first partial (not from +0: four adds fewer per quad; a partial
             // of −0 stays −0, which changes no MFMA product sum that is not exactly zero)
@@ -2541,13 +2557,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 by[0] += yp[sp];
                 b1 += f32x2{yq[sp].x, yq[sp].y};
             }
-            if constexpr (BLS) {  // the BLS direction carries no residual (the trials are evaluated exactly)
-                bt[0] = by[0];
-            } else {
+            if constexpr (WF) {
                 f32x4 bz = zq[0];
 #pragma unroll
                 for (int sp = 1; sp < kZS; ++sp) bz += zq[sp];
                 bt[0] = by[0] + bz;
+            } else {
+                bt[0] = by[0];
             }
             by[1] = bt[1] = f32x4{b1.x, b1.y, 0.f, 0.f};
         }
@@ -2557,8 +2573,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             if (i < KQ2) {
                 f32x4 bz = {0.f, 0.f, 0.f, 0.f};
                 for (int sp = 0; sp < nsplit; ++sp)
-                    by[i] += *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + cl) * ldy + i * 16 + r4x);
-                if (i == 0 && !BLS) {  // z has rank 16: rows 0-15 only (BLS: no residual in the direction)
+                    by[i] += *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + ycl) * ldy + i * 16 + r4y);
+                if (i == 0 && WF) {  // z has rank 16: rows 0-15 only
                     for (int sp = 0; sp < zsplit; ++sp)
                         bz += *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + r4x);
                 }
@@ -2574,33 +2590,33 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
             for (int m = 0; m < 4; ++m) {
 #pragma unroll
-                for (int j = 0; j < S2T; ++j)
+                for (int j = 0; j < (WF ? S2T : 0); ++j)
                     if (wave + j * nwaves < MT2)
                         acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2][m], bt[0][m], acc[j], 0, 0, 0);
 #pragma unroll
-                for (int g = 0; g < kGT; ++g)
+                for (int g = 0; g < (WG ? kGT : 0); ++g)
                     if (nwaves - 1 - wave + g * nwaves < kMTG)
                         ag[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(ga[g][0][m], by[0][m], ag[g], 0, 0, 0);
             }
 #pragma unroll
             for (int m = 0; m < 2; ++m)  // kR24
 #pragma unroll
-                for (int g = 0; g < kGT; ++g)
+                for (int g = 0; g < (WG ? kGT : 0); ++g)
                     if (nwaves - 1 - wave + g * nwaves < kMTG)
                         ag[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(ga[g][1][m], by[1][m], ag[g], 0, 0, 0);
 #pragma unroll
-            for (int j = 0; j < S2T; ++j)
+            for (int j = 0; j < (WF ? S2T : 0); ++j)
                 if (wave + j * nwaves < MT2)
                     *reinterpret_cast<f32x4*>(dP + cl * ldx + (wave + j * nwaves) * 16 + r4x) = acc[j];
 #pragma unroll
-            for (int g = 0; g < kGT; ++g) {
+            for (int g = 0; g < (WG ? kGT : 0); ++g) {
                 const int u = nwaves - 1 - wave + g * nwaves;
                 if (u < kMTG) *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4x) = ag[g];
             }
             return;
         }
 #pragma unroll
-        for (int j = 0; j < S2T; ++j) {
+        for (int j = 0; j < (WF ? S2T : 0); ++j) {
             if (wave + j * nwaves < MT2) {
 #pragma unroll
                 for (int m = 0; m < 4; ++m)
@@ -2608,12 +2624,12 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             }
         }
 #pragma unroll
-        for (int j = 0; j < S2T; ++j) {
+        for (int j = 0; j < (WF ? S2T : 0); ++j) {
             if (wave + j * nwaves < MT2)
                 *reinterpret_cast<f32x4*>(dP + cl * ldx + (wave + j * nwaves) * 16 + r4x) = acc[j];
         }
         // G tiles (waypoint rows of V_R·y''), from the top wave down
-        for (int u = nwaves - 1 - wave; u < MTG; u += nwaves) {
+        for (int u = nwaves - 1 - wave; WG && u < MTG; u += nwaves) {
             const f32x4* ap = reinterpret_cast<const f32x4*>(VN) + (size_t)u * KQ2 * 64 + lane;
             f32x4 ag = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -2626,22 +2642,6 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 }
             }
             *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4x) = ag;
-        }
-    };
-    // BLS trials: dP = F·z, z = V_Rᵀ·e (the trial iterate's rounding residual e, stage1z), the F tiles at
-    // rank 16 as in stage 2 — the waypoint image L·e of the residual (F·V_Rᵀ ≈ L on the rank-16 subspace,
-    // the rest below 1e-7 of |L·e|, see stage1z)
-    auto stage2z = [&]() {
-        f32x4 bz = *reinterpret_cast<const f32x4*>(Zp + cl * ldy + r4x);
-        for (int sp = 1; sp < zsplit; ++sp) bz += *reinterpret_cast<const f32x4*>(Zp + (sp * 16 + cl) * ldy + r4x);
-#pragma unroll
-        for (int j = 0; j < S2T; ++j) {
-            if (wave + j * nwaves < MT2) {
-                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                for (int m = 0; m < 4; ++m) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2][m], bz[m], acc, 0, 0, 0);
-                *reinterpret_cast<f32x4*>(dP + cl * ldx + (wave + j * nwaves) * 16 + r4x) = acc;
-            }
         }
     };
     // this lane's direction rows Δ = (F·y'')·J for waypoint j (the endpoint velocity rows are in y'')
@@ -2665,10 +2665,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         }
     };
     // G[n] = (V_R·y'')[n] (no mix: [a'; b'] carry Jᵀ; the endpoint velocity rows are in y'')
-    auto grad_alpha = [&](int j, float (&G)[D]) {
+    auto grad_alpha = [&](int j, float (&G)[D], int gt) {  // gt: the trajectory slot whose G is read
         const int r = wl[j] ? nn[j] : 0;  // (valid trajectories only)
 #pragma unroll
-        for (int k = 0; k < D; ++k) G[k] = Gb[(t * D + k) * lde + swz(r, t * D + k)];
+        for (int k = 0; k < D; ++k) G[k] = Gb[(gt * D + k) * lde + swz(r, gt * D + k)];
     };
     auto snapshot = [&](irm_stats& st) {  // extended-vis frame after a non-breaking inner iteration
         if (rec && st.series_len < P.max_series) {
@@ -2684,16 +2684,61 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         }
     };
 
+    // ---- BLS line-search helpers (kHelp, lean_help): when one trajectory t* of the workgroup is left in a
+    // line search, the first done slot evaluates its next trial (lr·β₋, optimizer_BLS.py:143-147) in the
+    // same round: a rejected trial changes nothing but lr, so the sequential search's decisions, counters
+    // and log are unchanged — only rounds are saved.  The helper reads t*'s α, T, V rows (ss, written by
+    // t* whenever they change) and scalars (hp, every round); its trial's direction folds its own residual
+    // into t*'s y'' (stage 2 reads t*'s Ypart columns for the helper's columns); every wave of both slots
+    // replays the decision; if the helper's trial is the accepted one, the helper writes t*'s gradient
+    // inputs and α, T, V, which t* adopts at the next round's start.
+    float* SS = smem + LX.ss;  // [3·D][MAXT]: α, T, V of the thread's waypoint
+    float* HP = smem + LX.hp;  // [slot][kHpW]: lr, ljl, lsg, loss, trial, inner, bfar (per wave of the slot)
+    constexpr int kSlots = (MAXT / 64) / WPTL;
+    auto ss_write = [&](int tt, const float (&a)[WPL][D], const float (&qq)[WPL][D], const float (&vv)[WPL][D]) {
+        const int th = tt * NWL + li;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            SS[k * MAXT + th] = a[0][k];
+            SS[(D + k) * MAXT + th] = qq[0][k];
+            SS[(2 * D + k) * MAXT + th] = vv[0][k];
+        }
+    };
+    auto ss_read = [&](int tt) {
+        const int th = tt * NWL + li;
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            al[0][k] = SS[k * MAXT + th];
+            q[0][k] = SS[(D + k) * MAXT + th];
+            v[0][k] = SS[(2 * D + k) * MAXT + th];
+        }
+    };
+    bool adopt = false;  // t*: the helper's trial was accepted — take its α, T, V at the next round's start
+
     // round 0 (optimizer_GD.py:93 / :210: the loss at α0) and the first gradient inputs
     irm_stats st{};
     st.series_len = rec ? 1 : 0;
+    auto write_out = [&]() {  // this trajectory's outputs: T, α, counters
+#pragma unroll
+        for (int j = 0; j < WPL; ++j) {
+            if (vl[j]) {
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    if (P.traj_out) P.traj_out[(b * N + nn[j]) * D + k] = q[j][k];
+                    if (P.alpha_out) P.alpha_out[(b * N + nn[j]) * D + k] = al[j][k];
+                }
+            }
+        }
+        if (P.stats && li == 0) P.stats[b] = st;
+    };
+
     float loss;
     bool done = !tvalid;
     {
         WP<D> w[WPL];
         evaluate(q, v, false, ljl, w);
         __syncthreads();
-        const Fin f = finalize(lsg);
+        const Fin f = finalize(lsg, t);
         loss = f.nl;
         if constexpr (!BLS) st.cost_evals = 1;
         bool to_end = P.max_inner <= 0;
@@ -2710,15 +2755,29 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             needs_dir = true;
         }
         if (!done && !to_end) {
-            bfar = grad_inputs(w, q, v, f.idx, lsg, ljl);
+            bfar = grad_inputs(w, q, v, f.idx, lsg, ljl, t);
             xdense = bfar;
+        }
+        if constexpr (kHelp) {
+            if (tvalid) {
+                ss_write(t, al, q, v);
+                if (n0 == 0 && lane == 0) {
+                    HP[t * kHpW + 0] = lr;
+                    HP[t * kHpW + 1] = ljl;
+                    HP[t * kHpW + 2] = lsg;
+                    HP[t * kHpW + 3] = loss;
+                    HP[t * kHpW + 4] = __int_as_float(0);
+                    HP[t * kHpW + 5] = __int_as_float(0);
+                }
+            }
         }
         if constexpr (GD1) {
             if (lane == 0 && (!done || bfar)) atomicOr(&fw[0], (done ? 0u : 1u << wave) | (bfar ? 1u << 31 : 0u));
         } else {
             if (lane == 0 && tvalid)
                 atomicOr(&fw[0], (1u << wave) | (needs_dir ? 1u << 28 : 0u) | (phase == LP_RESYNC ? 1u << 29 : 0u) |
-                                     (phase == LP_STEP ? 1u << 30 : 0u) | (bfar ? 1u << 31 : 0u));
+                                     (phase == LP_STEP ? 1u << 30 : 0u) |
+                                     ((BLS ? xdense && phase == LP_STEP : bfar) ? 1u << 31 : 0u));
         }
     }
     __syncthreads();
@@ -2728,17 +2787,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // (one L2 round trip per batch), so D = 3 with one waypoint per lane takes 8 rows per batch — no extra
     // spills there (C3 faithful 4.57 -> 4.42 ms, C3 BLS faithful 5.68 -> 5.60, C2 0.706 -> 0.689, same
     // box, same sums in the same order); the D = 7 / two-waypoint variants keep 2 (register peak)
+    constexpr bool kReloadOps = D > 3 && MAXT > 256;
 #ifndef IRM_X_RESYNC_U
     constexpr int kResyncU = (D <= 3 && WPL == 1) ? 8 : 2;
 #else
     constexpr int kResyncU = (D <= 3 && WPL == 1) ? IRM_X_RESYNC_U : 2;
 #endif
     // ---------------------------------------------------------- rounds
-    float dTl[BLS ? WPL : 1][D], dVl[BLS ? WPL : 1][D], Gl[BLS ? WPL : 1][D];  // BLS: latched direction
-#pragma unroll
-    for (int j = 0; j < (BLS ? WPL : 1); ++j)
-#pragma unroll
-        for (int k = 0; k < D; ++k) dTl[j][k] = dVl[j][k] = Gl[j][k] = 0.f;
     // The second half of the waves (4-7: the younger partner on each SIMD) loses VALU arbitration to
     // the older one in every phase; static priority for that half (MI355X_MICROARCH.md, two waves per
     // SIMD, item 4): C3 +1.7 %.  Priority only reorders issue: results are unchanged.
@@ -2757,6 +2812,48 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         const bool dirr = GD1 || ((fl >> 28) & 1u);  // some trajectory needs a direction this round
         const bool rsy = !GD1 && ((fl >> 29) & 1u);  // some trajectory ends an inner loop this round
         if (tid == 0) fw[par ^ 1] = 0u;
+        bool hm = false, helper = false;  // helper round (block-uniform) / this wave helps
+        int ts = 0, hs = 0;               // t*, the helper slot
+        float h_lr0 = 0.f, h_lr = 0.f, h_ljl = 0.f, h_lsg = 0.f, h_loss = 0.f, h_gn = 1.f, h_an = 0.f;
+        int h_trial = 0, h_inner = 0;
+        if constexpr (kHelp) {
+            if (adopt) {  // t*: the previous round accepted the helper's trial
+                ss_read(t);
+                xdense = HP[t * kHpW + 6 + (wave - t * WPTL)] != 0.f;
+                adopt = false;
+            }
+            if (!rec && !P.lean_nohelp && ((fl >> 30) & 1u) && kSlots > 1) {
+                unsigned live = 0u;
+#pragma unroll
+                for (int s2 = 0; s2 < kSlots; ++s2)
+                    if ((fl >> (s2 * WPTL)) & ((1u << WPTL) - 1u)) live |= 1u << s2;
+                if (__builtin_popcount(live) == 1) {
+                    hm = true;
+                    ts = __builtin_ctz(live);
+                    hs = ts == 0 ? 1 : 0;
+                    helper = t == hs;
+                }
+            }
+            ycl = (hm && cl / D == hs) ? ts * D + cl % D : cl;
+            r4y = r4 ^ (ycl & 4);
+            if (helper) {  // wave-uniform: t*'s state and scalars (its own trajectory is done and written out)
+                ss_read(ts);
+                const size_t bs = (size_t)(tb0 + ts);
+#pragma unroll
+                for (int k = 0; k < D; ++k) tg[0][k] = (nn[0] == N - 1) ? P.goal[bs * D + k] : P.start[bs * D + k];
+                vl[0] = wl[0];
+                obs = obsL + (P.obs_stride ? ts * obs_pitch(P.O) : 0);  // t*'s obstacles (per-problem sets)
+                h_lr0 = HP[ts * kHpW + 0];
+                h_lr = h_lr0 * P.bls_bm;
+                h_ljl = HP[ts * kHpW + 1];
+                h_lsg = HP[ts * kHpW + 2];
+                h_loss = HP[ts * kHpW + 3];
+                // (a direction round of t* — the only live trajectory, so dirr is its own — resets its trial
+                // count at the inner-loop head, after HP was written)
+                h_trial = dirr ? 0 : __float_as_int(HP[ts * kHpW + 4]);
+                h_inner = __float_as_int(HP[ts * kHpW + 5]);
+            }
+        }
         IRM_STAMP(0);
         if (dirr) {  // block-uniform
             IRM_COUNT(13, dense);
@@ -2790,19 +2887,14 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     }
                 }
             }
-            stage2();
+            stage2f(std::bool_constant<!BLS>{}, std::true_type{});  // (BLS: G only; F below, per trial)
             IRM_STAMP(3);
             __syncthreads();
             IRM_STAMP(4);
         }
-        // ------------------------------------------------ BLS: latch the direction
+        // ------------------------------------------------ BLS: a new direction (the inner-loop head)
         if constexpr (BLS) {
-            if (needs_dir) {  // wave-uniform; the inner-loop head (optimizer_BLS.py:163-166)
-#pragma unroll
-                for (int j = 0; j < WPL; ++j) {
-                    direction(j, dTl[j], dVl[j]);  // (F·y'')·J = L·G·J
-                    grad_alpha(j, Gl[j]);
-                }
+            if (needs_dir) {  // wave-uniform; optimizer_BLS.py:163-166
                 gnorm = sqrtf(wp[t * 2]);
                 anorm = wp[t * 2 + 1] / gnorm;
                 st.grad_evals++;  // cost + grad at α (optimizer_BLS.py:163-164)
@@ -2811,12 +2903,17 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 needs_dir = false;
             }
         }
-        // this round's step (BLS: the trial's)
-        float cj = cfac, stepj = lr;
-        const float lrj = lr;
+        // this round's step (BLS: the trial's; a helper's: t*'s next trial, lr·β₋)
+        float cj = cfac, stepj = lr, lrj = lr, gnj = gnorm;
         if constexpr (BLS) {
-            cj = unfused(1.f - unfused(P.lreg * lr));  // (1 − λ_reg·bls_lr) in fp32 (optimizer_BLS.py:139)
-            stepj = lr / gnorm;
+            if (helper) {
+                h_gn = sqrtf(wp[ts * 2]);  // t*'s ‖G‖ and alpha_norm, the same expressions as t*'s latch
+                h_an = wp[ts * 2 + 1] / h_gn;
+                lrj = h_lr;
+                gnj = h_gn;
+            }
+            cj = unfused(1.f - unfused(P.lreg * lrj));  // (1 − λ_reg·bls_lr) in fp32 (optimizer_BLS.py:139)
+            stepj = lrj / gnj;
         }
         // ------------------------------------------------ BLS: the trial's fp32 iterate and its trajectory
         // The reference evaluates each trial at its own fp32 iterate α_j = fl(fl(c_j·α) − fl(lr_j·ĝ))
@@ -2825,28 +2922,37 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         // iterate's rounding residual e_j = α_j − (c_j·α − s_j·G) (alpha_step, error-free): e_j goes
         // through z = V_Rᵀ·e_j and F·z (rank 16) before the evaluation, so the trial is evaluated at α_j's
         // own trajectory to fp32 resolution — not one rounding residual behind it.
+        // The residual enters the direction like the GD flows' (scaled by −1/s_j, stage 2's z): the trial's
+        // direction F·(y'' + z_j) with z_j = −V_Rᵀ·e_j/s_j, so c_j·[T; V] − s_j·(direction)·J is the
+        // trial's trajectory.  G comes from Gb, which every stage 2 rewrites with the same values for a
+        // trajectory in its line search (its gradient inputs in X are unchanged, and the stage-1 velocity
+        // half runs whenever a live trajectory's inputs have one, the dense flag): no per-lane latches.
         float aj[BLS ? WPL : 1][D];
         if constexpr (BLS) {
             if ((fl >> 30) & 1u) {  // block-uniform: some trajectory has a line-search trial this round
-                if (phase == LP_STEP) {  // wave-uniform
+                if (phase == LP_STEP || helper) {  // wave-uniform
+                    const float ne = -1.f / fmaxf(stepj, kMinRefStep);
 #pragma unroll
                     for (int j = 0; j < WPL; ++j) {
-                        float er[D];
+                        float G[D], eo[D];
+                        grad_alpha(j, G, helper ? ts : t);
 #pragma unroll
                         for (int k = 0; k < D; ++k) {
-                            const float gh = Gl[j][k] / gnorm;  // n_alpha_grad (optimizer_BLS.py:165)
-                            aj[j][k] = alpha_step(al[j][k], cj, lrj, gh, stepj, Gl[j][k], er[k]);
+                            const float gh = G[k] / gnj;  // n_alpha_grad (optimizer_BLS.py:165)
+                            float er;
+                            aj[j][k] = alpha_step(al[j][k], cj, lrj, gh, stepj, G[k], er);
+                            eo[k] = er * ne;
                         }
-                        if (vl[j]) {
+                        if (wl[j]) {
 #pragma unroll
-                            for (int k = 0; k < D; ++k) Eb[(t * D + k) * lde + swz(nn[j], t * D + k)] = er[k];
+                            for (int k = 0; k < D; ++k) Eb[(t * D + k) * lde + swz(nn[j], t * D + k)] = eo[k];
                         }
                     }
                 }
                 __syncthreads();
                 stage1z();
                 __syncthreads();
-                stage2z();
+                stage2f(std::true_type{}, std::false_type{});
                 __syncthreads();
             }
         }
@@ -2881,27 +2987,25 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     }
                 }
             }
+            // the operator fragments again (from L2): so they are not live across the resync's exact
+            // evaluation, whose register peak spilled them (the 7-DoF dual-loop / BLS kernels)
+            if constexpr (kReloadOps) {
+                asm volatile("" ::: "memory");
+                load_ops();
+            }
             __syncthreads();  // X is rewritten by this round's gradient inputs
         }
         // ------------------------------------------------ update + evaluate
         float q2[WPL][D], v2[WPL][D];
         WP<D> w[WPL];
-        const bool stepping = GD1 ? !done : phase == LP_STEP;  // wave-uniform
-        const bool ev = GD1 ? !done : phase != LP_DONE;
+        const bool stepping = GD1 ? !done : (phase == LP_STEP || helper);  // wave-uniform
+        const bool ev = GD1 ? !done : (phase != LP_DONE || helper);
         if (ev) {
 #pragma unroll
             for (int j = 0; j < WPL; ++j) {
                 if (stepping) {
                     float dt[D], dv[D];
-                    if constexpr (BLS) {
-                        float ct[D], cv[D];
-                        direction(j, ct, cv);  // (F·z)·J = L·e_j·J, the trial iterate's rounding residual
-#pragma unroll
-                        for (int k = 0; k < D; ++k) {
-                            q2[j][k] = fmaf(cj, q[j][k], -(stepj * dTl[j][k])) + ct[k];
-                            v2[j][k] = fmaf(cj, v[j][k], -(stepj * dVl[j][k])) + cv[k];
-                        }
-                    } else {
+                    {
                         direction(j, dt, dv);
 #pragma unroll
                         for (int k = 0; k < D; ++k) {
@@ -2937,20 +3041,40 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             // an inner loop's end is evaluated with the next outer iteration's λ (its loss and gradient
             // start that iteration; the constraint terms do not depend on λ)
             const bool rs = !GD1 && phase == LP_RESYNC;
-            evaluate(q2, v2, rs, rs ? ljl * P.lci : ljl, w);
+            evaluate(q2, v2, rs, helper ? h_ljl : rs ? ljl * P.lci : ljl, w);
         }
         IRM_STAMP(7);
         if constexpr (WPTL > 1) {
             __syncthreads();  // the trajectory's wave partials come from several waves
+        } else if (hm) {      // block-uniform: t* reads the helper's records
+            __syncthreads();
         } else {              // one wave per trajectory: its own LDS writes, in order
             __builtin_amdgcn_wave_barrier();
             asm volatile("" ::: "memory");
         }
         IRM_STAMP(8);
-        if (ev) {
+        if constexpr (kHelp) {
+            if (helper) {  // replay t*'s decision up to this trial: is it the accepted one?
+                const Fin f0 = finalize(h_lsg, ts);
+                if (f0.nl > h_loss - P.bls_a * h_lr0 * h_an && h_trial + 1 < P.max_bls) {
+                    const Fin f1 = finalize(h_lsg, t);
+                    if (!(f1.nl > h_loss - P.bls_a * h_lr * h_an)) {
+                        ss_write(ts, aj, q2, v2);  // t*'s α_j, T, V (adopted at the next round's start)
+                        if (!(h_loss - f1.nl < P.llr) && h_inner + 1 < P.max_inner) {
+                            const bool bf = grad_inputs(w, q2, v2, f1.idx, h_lsg, h_ljl, ts);  // t*'s columns
+                            if (lane == 0) {
+                                HP[ts * kHpW + 6 + (wave - t * WPTL)] = bf ? 1.f : 0.f;
+                                if (bf) atomicOr(&fw[par ^ 1], 1u << 31);
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        if (ev && !helper) {
             const bool rs = !GD1 && phase == LP_RESYNC;
             const float lsg_e = rs ? lsg * P.lci : lsg;
-            const Fin f = finalize(lsg_e);
+            const Fin f = finalize(lsg_e, t);
             IRM_STAMP(9);
             bool bfar = false, to_end = false, accept = false, snap = false, more = false;
             if constexpr (!BLS) needs_dir = false;  // GD: every step consumes its direction
@@ -3011,34 +3135,45 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     else more = true;
                 }
             } else {  // BLS trial (optimizer_BLS.py:136-150, 172-178)
-                st.cost_evals++;
-                st.bls_trials++;
-                const float required = loss - P.bls_a * lr * anorm;
-                if (P.trace && b == 0 && li == 0 && st.bls_trials - 1 < P.trace_cap) {  // line-search log
-                    float* r = P.trace + (size_t)(st.bls_trials - 1) * kTraceW;
-                    r[0] = (float)outer;
-                    r[1] = (float)inner;
-                    r[2] = (float)trial;
-                    r[3] = lr;
-                    r[4] = f.nl;
-                    r[5] = required;
-                    r[6] = (f.nl > required) ? 0.f : 1.f;
-                    r[7] = loss;
-                    r[8] = gnorm;
-                    r[9] = anorm;
-                }
                 bool inner_end = false, rejected_all = false;
                 float improve = 0.f;
-                if (f.nl > required) {
-                    lr = lr * P.bls_bm;
-                    trial++;
-                    if (trial >= P.max_bls) inner_end = rejected_all = true;  // new_loss = loss
-                } else {
-                    accept = true;
-                    lr = lr * P.bls_bp;
-                    improve = loss - f.nl;
-                    loss = f.nl;
-                    inner_end = true;
+                // this round's trials in the sequential order: t*'s own, then (helper round) the helper's
+#pragma unroll
+                for (int kk = 0; kk < (kHelp ? 2 : 1); ++kk) {
+                    if (kk == 1 && (!hm || accept || inner_end)) break;  // (the helper's trial was not reached)
+                    const Fin fk = kk == 0 ? f : finalize(lsg_e, hs);
+                    st.cost_evals++;
+                    st.bls_trials++;
+                    const float required = loss - P.bls_a * lr * anorm;
+                    if (P.trace && b == (size_t)(P.trace_b & 0xFFFFFF) && li == 0 && st.bls_trials - 1 < P.trace_cap) {  // line-search log
+                        float* r = P.trace + (size_t)(st.bls_trials - 1) * kTraceW;
+                        r[0] = (float)outer;
+                        r[1] = (float)inner;
+                        r[2] = (float)trial;
+                        r[3] = lr;
+                        r[4] = fk.nl;
+                        r[5] = required;
+                        r[6] = (fk.nl > required) ? 0.f : 1.f;
+                        r[7] = loss;
+                        r[8] = gnorm;
+                        r[9] = anorm;
+                        if (P.trace_b >> 30) {  // diagnostics: helper round (outer + 100), helper's trial (trial + 1000)
+                            if (hm) r[0] += 100.f;
+                            if (kk == 1) r[2] += 1000.f;
+                        }
+                    }
+                    if (fk.nl > required) {
+                        lr = lr * P.bls_bm;
+                        trial++;
+                        if (trial >= P.max_bls) inner_end = rejected_all = true;  // new_loss = loss
+                    } else {
+                        if (kk == 0) accept = true;
+                        else adopt = true;  // the helper's α_j and trajectory, next round
+                        lr = lr * P.bls_bp;
+                        improve = loss - fk.nl;
+                        loss = fk.nl;
+                        inner_end = true;
+                    }
                 }
                 if (inner_end) {
                     if (improve < P.llr) {
@@ -3075,7 +3210,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
                 for (int j = 0; j < WPL; ++j) {
                     float G[D];
-                    grad_alpha(j, G);
+                    grad_alpha(j, G, t);
                     // the D element chains first (one basic block, interleaved), then the residual stores
                     float eo[D];
 #pragma unroll
@@ -3098,19 +3233,39 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 phase = LP_RESYNC;
             }
             if constexpr (GD1) {
-                if (more) bfar = grad_inputs(w, q2, v2, f.idx, lsg, ljl);
+                if (more) bfar = grad_inputs(w, q2, v2, f.idx, lsg, ljl, t);
                 if (lane == 0 && (!done || bfar))
                     atomicOr(&fw[par ^ 1], (done ? 0u : 1u << wave) | (bfar ? 1u << 31 : 0u));
             } else {
                 if (more) {
-                    bfar = grad_inputs(w, q2, v2, f.idx, lsg, ljl);
-                    xdense = bfar;
+                    if (!(kHelp && adopt)) {  // (adopted: the helper wrote the gradient inputs)
+                        bfar = grad_inputs(w, q2, v2, f.idx, lsg, ljl, t);
+                        xdense = bfar;
+                    }
                     needs_dir = true;
+                }
+                if constexpr (kHelp) {
+                    // publish this trajectory's state for a helper: α, T, V when they changed (an accepted
+                    // trial of its own, a new outer iteration's exact trajectory), the scalars every round
+                    if (phase == LP_STEP && (accept || rs)) ss_write(t, al, q, v);
+                    if (phase != LP_DONE && n0 == 0 && lane == 0) {
+                        HP[t * kHpW + 0] = lr;
+                        HP[t * kHpW + 1] = ljl;
+                        HP[t * kHpW + 2] = lsg;
+                        HP[t * kHpW + 3] = loss;
+                        HP[t * kHpW + 4] = __int_as_float(trial);
+                        HP[t * kHpW + 5] = __int_as_float(inner);
+                    }
+                    // done: the outputs now (this slot's registers may serve as a helper from here on)
+                    if (phase == LP_DONE && tvalid) write_out();
                 }
                 if (lane == 0 && phase != LP_DONE)
                     atomicOr(&fw[par ^ 1], (1u << wave) | (needs_dir ? 1u << 28 : 0u) |
                                                (phase == LP_RESYNC ? 1u << 29 : 0u) | (phase == LP_STEP ? 1u << 30 : 0u) |
-                                               (bfar ? 1u << 31 : 0u));
+                                               // BLS: every trajectory in a line search keeps the velocity
+                                               // half on while its inputs have one (its Ypart / Gb columns
+                                               // are recomputed by other trajectories' direction rounds)
+                                               ((BLS ? xdense && phase == LP_STEP : bfar) ? 1u << 31 : 0u));
             }
         }
         IRM_STAMP(11);
@@ -3140,27 +3295,16 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         }
         __syncthreads();
         if (tvalid) {
-            const Fin f = finalize(lsg);
+            const Fin f = finalize(lsg, t);
             const bool ok = sqrtf(f.a0) < P.eps_p && sqrtf(f.a1) < P.eps_p && sqrtf(f.b0) < P.eps_v &&
                             sqrtf(f.b1) < P.eps_v && f.tx <= P.pmax && f.tn >= P.pmin && f.va <= P.vmax;
             st.outer_iterations = 1;
             st.constraints_ok = ok ? 1 : 0;
         }
     }
-    // (LF_GD2 / LF_BLS: every trajectory ended through LP_RESYNC — q, v are α's exact trajectory)
-    if (tvalid) {
-#pragma unroll
-        for (int j = 0; j < WPL; ++j) {
-            if (vl[j]) {
-#pragma unroll
-                for (int k = 0; k < D; ++k) {
-                    if (P.traj_out) P.traj_out[(b * N + nn[j]) * D + k] = q[j][k];
-                    if (P.alpha_out) P.alpha_out[(b * N + nn[j]) * D + k] = al[j][k];
-                }
-            }
-        }
-        if (P.stats && li == 0) P.stats[b] = st;
-    }
+    // (LF_GD2 / LF_BLS: every trajectory ended through LP_RESYNC — q, v are α's exact trajectory;
+    // kHelp: written when the trajectory finished)
+    if (!kHelp && tvalid) write_out();
     if (tid == 0) prof.flush(P.prof);
 }
 
@@ -3290,10 +3434,11 @@ struct type_tag {
 };
 
 // LDS of k_lean: the optimiser head + obstacles, no staged F fragments, the lean regions.
-inline size_t lean_lds(const KParams& p) {
+inline size_t lean_lds(const KParams& p, bool help = false) {
     KParams q = p;
     q.regops = 1;
-    return (size_t)lean_extra(plan_lds(q, false, true, true).total, p.MP, p.NK, p.RP, p.nsplit, lean_vlds(p.NK, p.D, p.BT)).total * 4;
+    return (size_t)lean_extra(plan_lds(q, false, true, true).total, p.MP, p.NK, p.RP, p.nsplit, lean_vlds(p.NK, p.D, p.BT),
+                              p.D, help ? p.BT : 0).total * 4;
 }
 
 // The lean kernel's control flow for a launch (-1: the general kernel serves it): the GD single
@@ -3353,7 +3498,7 @@ hipError_t launch_lean_one(const KParams& p, int grid, hipStream_t s, LaunchDesc
         desc->rank_z = desc->rank_dir = 16;  // k_lean's per-stage ranks at RP = 32
         desc->rank_g = 24;
     }
-    return run_optimizer(desc, k_lean<Sh, TT, WPL, FULL, FLOW>, grid, p.BT, lean_lds(p), s, p);
+    return run_optimizer(desc, k_lean<Sh, TT, WPL, FULL, FLOW>, grid, p.BT, lean_lds(p, lean_help<Sh, TT, WPL, FULL, FLOW>()), s, p);
 }
 
 template <class Sh, int TT, int WPL, bool FULL>

@@ -886,6 +886,31 @@ def test_batched_flows_independent_of_workgroup_neighbours(cfg, flow, faithful):
           f"max {ref[2]['grad_evals'].max()}, trials {ref[2]['bls_trials'].sum()}")
 
 
+@pytest.mark.parametrize("cfg", ["c3bls", "c2"])
+def test_bls_line_search_helpers_change_nothing(cfg, monkeypatch):
+    """k_lean's BLS line-search helpers (a done slot evaluates the last live trajectory's next trial in the
+    same round) only save rounds: α, trajectory, every statistic and the line-search log of
+    batch index 0 are bit-identical with the helpers switched off (IRM_LEAN_NOHELP=1).  C3-BLS: 64 problems
+    at four per workgroup (helpers in every workgroup's tail); C2: one trajectory, helpers from round 0."""
+    import bench
+    s, g, obs = bench.make_problem(cfg, 1, 0)
+    B = 64 if cfg == "c3bls" else 1
+    s, g = s[:B], g[:B]
+    outs = []
+    for off in ("1", "0"):
+        monkeypatch.setenv("IRM_LEAN_NOHELP", off)
+        c = _flow_ctx(cfg, 4 if cfg == "c3bls" else 0, True)
+        assert c.launch_plan(B, len(obs))["kernel"].startswith("k_lean<FixShape<3,128,32>,512,1,FULL,BLS>"), \
+            c.launch_plan(B, len(obs))
+        c.bls_trace_enable(4096)
+        a, t, st = c.optimize(s, g, obs)
+        outs.append((a, t, st, c.bls_trace(int(st["bls_trials"][0]))))
+    (a0, t0, st0, tr0), (a1, t1, st1, tr1) = outs
+    _assert_same((a1, t1, st1), (a0, t0, st0), f"{cfg}: helpers on vs off")
+    np.testing.assert_array_equal(tr1, tr0)
+    print(f"{cfg}: {int(st0['bls_trials'].sum())} trials, log of problem 0: {len(tr0)} rows, identical")
+
+
 def test_batched_bls_line_search_follows_oracle():
     """The BLS line search of three C3 problems, each traced while it shares a four-trajectory workgroup
     (it is moved to batch index 0, which the line-search log records): the first 4 inner iterations
