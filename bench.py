@@ -98,7 +98,7 @@ def make_args(cfg, faithful, max_inner):
     return irm_main.parse_args(argv)
 
 
-def flops_per_iteration(N, D, O, R, split=False, lean=True, ranks=None):
+def flops_per_iteration(N, D, O, R, split=False, lean=True, ranks=None, bls=False):
     """Algorithmic fp32 flops of one GD iteration of one trajectory.
 
     exec: what the optimiser kernel (waypoint-space rank-R iteration with the reference's fp32 α
@@ -106,16 +106,25 @@ def flops_per_iteration(N, D, O, R, split=False, lean=True, ranks=None):
     (2·Rz·N·D), stage 2 (the direction F·(y'' + z), 2·2N·Rf·D; G = V_R·y'', 2·N·Rg·D) — k_lean at
     R = 32 runs z and the direction at rank 16 and G at rank 24, k_optimize all at
     R —, the Jᵀ / J mixes of the gradient inputs and of the direction (2 × 2·2·N·D²), the α update
-    with its error-free residual (14·N·D), the waypoint update (4·N·D), obstacle pairs (14·N·O),
-    FK / Jacobian / penalties (24·N·D, sincos counted as 4 flops each).
+    with its residual (k_lean's two-FMA form 7·N·D, k_optimize's error-free one 14·N·D), the waypoint
+    update (4·N·D), obstacle pairs (14·N·O), FK / Jacobian / penalties (24·N·D, sincos counted as 4 flops
+    each).
     ref: SURVEY.md §8d's count of the reference formulation, 12N²D + 10ND² + 22NO.
-    split: (direction round, trial round) — a BLS inner iteration is one direction round (the MFMA
-    stages, the mixes, the α update of the accepted step) and one evaluation per line-search trial
-    (waypoint update, obstacle pairs, FK / Jacobian / penalties); GD = one of each.
+    split: (direction round, trial round) — a BLS inner iteration is one direction round and one trial
+    round per line-search trial; GD = one of each.  k_lean's BLS (bls=True): the direction round is
+    stage 1, G and the gradient-input mix; every trial forms its fp32 iterate with the exact residual
+    (14·N·D), projects the residual (z, 2·Rz·N·D) and runs the F tiles and the direction mix before its
+    evaluation (round 4: each trial evaluated at its own iterate).
     """
     Rz, Rf, Rg = ranks if ranks is not None else ((16, 16, 24) if (lean and R == 32) else (R, R, R))
-    dir_f = 2 * R * N * D + 2 * Rz * N * D + 4 * Rf * N * D + 2 * Rg * N * D + 8 * N * D * D + 14 * N * D
-    trial_f = 4 * N * D + 14 * N * O + 24 * N * D
+    ev_f = 4 * N * D + 14 * N * O + 24 * N * D
+    if bls and lean:
+        dir_f = 2 * R * N * D + 2 * Rg * N * D + 4 * N * D * D
+        trial_f = 14 * N * D + 2 * Rz * N * D + 4 * Rf * N * D + 4 * N * D * D + ev_f
+    else:
+        dir_f = (2 * R * N * D + 2 * Rz * N * D + 4 * Rf * N * D + 2 * Rg * N * D + 8 * N * D * D
+                 + (7 if lean else 14) * N * D)
+        trial_f = ev_f
     ref_f = 12 * N * N * D + 10 * N * D * D + 22 * N * O
     if split:
         return dir_f, trial_f, ref_f
@@ -428,7 +437,9 @@ def main():
 
     plan = ctx.launch_plan(B, O)
     kernel = plan_label(plan)
-    dir_f, trial_f, ref_f = flops_per_iteration(N, D, O, info["operator_rank"], split=True, ranks=(plan["rank_z"], plan["rank_dir"], plan["rank_g"]))
+    dir_f, trial_f, ref_f = flops_per_iteration(N, D, O, info["operator_rank"], split=True, lean=bool(plan["lean"]),
+                                                ranks=(plan["rank_z"], plan["rank_dir"], plan["rank_g"]),
+                                                bls=opt == "bls")
     exec_f = dir_f + trial_f
     # GD: one trial per iteration; BLS: the trials the line searches ran
     launch_flops = dir_f * iters_rank + trial_f * (trials_rank if opt == "bls" else iters_rank)

@@ -2714,6 +2714,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         }
     };
     bool adopt = false;  // t*: the helper's trial was accepted — take its α, T, V at the next round's start
+    float aj[BLS ? WPL : 1][D];  // BLS: the trial's fp32 iterate α_j
+#pragma unroll
+    for (int k = 0; k < D; ++k) aj[0][k] = 0.f;
+    bool pre_eb = false;  // BLS: this trajectory's next trial iterate and residual are formed already
+    int n_rounds = 0, n_hm = 0;  // diagnostics (trace_b bit 29): kernel rounds / helper rounds until this trajectory ended
 
     // round 0 (optimizer_GD.py:93 / :210: the loss at α0) and the first gradient inputs
     irm_stats st{};
@@ -2776,7 +2781,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         } else {
             if (lane == 0 && tvalid)
                 atomicOr(&fw[0], (1u << wave) | (needs_dir ? 1u << 28 : 0u) | (phase == LP_RESYNC ? 1u << 29 : 0u) |
-                                     (phase == LP_STEP ? 1u << 30 : 0u) |
+                                     (phase == LP_STEP ? (BLS ? (1u << 30) | (1u << 27) : 1u << 30) : 0u) |
                                      ((BLS ? xdense && phase == LP_STEP : bfar) ? 1u << 31 : 0u));
         }
     }
@@ -2817,6 +2822,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         float h_lr0 = 0.f, h_lr = 0.f, h_ljl = 0.f, h_lsg = 0.f, h_loss = 0.f, h_gn = 1.f, h_an = 0.f;
         int h_trial = 0, h_inner = 0;
         if constexpr (kHelp) {
+            n_rounds++;
             if (adopt) {  // t*: the previous round accepted the helper's trial
                 ss_read(t);
                 xdense = HP[t * kHpW + 6 + (wave - t * WPTL)] != 0.f;
@@ -2829,8 +2835,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     if ((fl >> (s2 * WPTL)) & ((1u << WPTL) - 1u)) live |= 1u << s2;
                 if (__builtin_popcount(live) == 1) {
                     hm = true;
+                    n_hm++;
                     ts = __builtin_ctz(live);
-                    hs = ts == 0 ? 1 : 0;
+                    // the neighbouring slot: the other SIMD pair (slot s = waves 2s, 2s+1 → SIMDs 2s mod 4,
+                    // 2s+1 mod 4 at two waves per slot), so the helper's VALU does not share t*'s SIMDs
+                    hs = ts ^ 1;
                     helper = t == hs;
                 }
             }
@@ -2927,10 +2936,12 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         // trial's trajectory.  G comes from Gb, which every stage 2 rewrites with the same values for a
         // trajectory in its line search (its gradient inputs in X are unchanged, and the stage-1 velocity
         // half runs whenever a live trajectory's inputs have one, the dense flag): no per-lane latches.
-        float aj[BLS ? WPL : 1][D];
         if constexpr (BLS) {
             if ((fl >> 30) & 1u) {  // block-uniform: some trajectory has a line-search trial this round
-                if (phase == LP_STEP || helper) {  // wave-uniform
+                // (a trial that continues a line search had its iterate and residual formed at the end of the
+                // last round, before its barrier: the first barrier below runs only when some trajectory
+                // forms its trial here — a new direction's first trial (flag bit 27) or a helper)
+                if ((phase == LP_STEP && !pre_eb) || helper) {  // wave-uniform
                     const float ne = -1.f / fmaxf(stepj, kMinRefStep);
 #pragma unroll
                     for (int j = 0; j < WPL; ++j) {
@@ -2949,7 +2960,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                         }
                     }
                 }
-                __syncthreads();
+                pre_eb = false;
+                if (((fl >> 27) & 1u) || hm) __syncthreads();
                 stage1z();
                 __syncthreads();
                 stage2f(std::true_type{}, std::false_type{});
@@ -3244,6 +3256,28 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     }
                     needs_dir = true;
                 }
+                if constexpr (BLS) {
+                    // a rejected trial continues the line search: the next trial's iterate and residual now,
+                    // before the round's last barrier (optimizer_BLS.py:139-140 at lr·β₋; no barrier for them
+                    // at the next round's start)
+                    if (phase == LP_STEP && !needs_dir && !(kHelp && adopt)) {
+                        const float cn = unfused(1.f - unfused(P.lreg * lr)), sn = lr / gnorm;
+                        const float ne = -1.f / fmaxf(sn, kMinRefStep);
+                        float G[D], eo[D];
+                        grad_alpha(0, G, t);
+#pragma unroll
+                        for (int k = 0; k < D; ++k) {
+                            float er;
+                            aj[0][k] = alpha_step(al[0][k], cn, lr, G[k] / gnorm, sn, G[k], er);
+                            eo[k] = er * ne;
+                        }
+                        if (wl[0]) {
+#pragma unroll
+                            for (int k = 0; k < D; ++k) Eb[(t * D + k) * lde + swz(nn[0], t * D + k)] = eo[k];
+                        }
+                        pre_eb = true;
+                    }
+                }
                 if constexpr (kHelp) {
                     // publish this trajectory's state for a helper: α, T, V when they changed (an accepted
                     // trial of its own, a new outer iteration's exact trajectory), the scalars every round
@@ -3257,11 +3291,15 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                         HP[t * kHpW + 5] = __int_as_float(inner);
                     }
                     // done: the outputs now (this slot's registers may serve as a helper from here on)
-                    if (phase == LP_DONE && tvalid) write_out();
+                    if (phase == LP_DONE && tvalid) {
+                        if ((P.trace_b >> 29) & 1) st.series_len = n_rounds | (n_hm << 16);  // diagnostics
+                        write_out();
+                    }
                 }
                 if (lane == 0 && phase != LP_DONE)
                     atomicOr(&fw[par ^ 1], (1u << wave) | (needs_dir ? 1u << 28 : 0u) |
                                                (phase == LP_RESYNC ? 1u << 29 : 0u) | (phase == LP_STEP ? 1u << 30 : 0u) |
+                                               (BLS && phase == LP_STEP && !pre_eb ? 1u << 27 : 0u) |
                                                // BLS: every trajectory in a line search keeps the velocity
                                                // half on while its inputs have one (its Ypart / Gb columns
                                                // are recomputed by other trajectories' direction rounds)

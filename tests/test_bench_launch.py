@@ -61,6 +61,10 @@ def test_bls_flop_model_counts_trials():
     e, ref2 = bench.flops_per_iteration(128, 3, 11, 32)
     assert e == d + t and ref == ref2
     assert t == 4 * 128 * 3 + 14 * 128 * 11 + 24 * 128 * 3  # update + obstacle pairs + FK / penalties
+    # k_lean's BLS: every trial also forms its iterate, projects its residual and runs the F tiles
+    db, tb, _ = bench.flops_per_iteration(128, 3, 11, 32, split=True, bls=True)
+    assert db == (2 * 32 + 2 * 24) * 128 * 3 + 4 * 128 * 9
+    assert tb == t + (14 + 2 * 16 + 4 * 16) * 128 * 3 + 4 * 128 * 9
 
 
 def test_cpu_baseline_runs_before_process_group_init(monkeypatch):

@@ -110,7 +110,8 @@ def test_bench_flop_model():
     assert ref_f == 12 * 128 * 128 * 3 + 10 * 128 * 9 + 22 * 128 * 11 == 632320
     assert 0 < exec_f < ref_f
     # k_lean at R = 32: stage 1 rank 32, residual z and direction rank 16, G rank 24
-    assert exec_f == (2 * 32 + 2 * 16 + 4 * 16 + 2 * 24) * 128 * 3 + 8 * 128 * 9 + 42 * 128 * 3 + 14 * 128 * 11 == 124928
+    # (the α update: k_lean's two-FMA residual, 7·N·D)
+    assert exec_f == (2 * 32 + 2 * 16 + 4 * 16 + 2 * 24) * 128 * 3 + 8 * 128 * 9 + 35 * 128 * 3 + 14 * 128 * 11 == 122240
     gen_f, _ = bench.flops_per_iteration(128, 3, 11, 32, lean=False)  # k_optimize: every stage at R
     assert gen_f == 10 * 32 * 128 * 3 + 8 * 128 * 9 + 42 * 128 * 3 + 14 * 128 * 11 == 167936
 
@@ -126,7 +127,7 @@ def test_bench_kernel_label_is_the_library_plan():
     assert "4 trajectories per 512-thread workgroup" in lab and "16/16/24" in lab
     f1, _ = bench.flops_per_iteration(128, 3, 11, 32, ranks=(16, 16, 24))
     f2, _ = bench.flops_per_iteration(128, 3, 11, 32)
-    assert f1 == f2 == 124928
+    assert f1 == f2 == 122240
 
 
 def test_bench_args_bench_mode():
