@@ -677,13 +677,18 @@ __device__ void stage_alpha(const KParams& P, int tb0, int ntb, float* X, int xr
 // U: K / dK rows per software-pipelined batch (8 in the prologue / epilogue; the optimiser loop's resync
 // rounds use 2, which keeps the register peak of the dual-loop / BLS instantiations low — spill-free —
 // at the cost of less latency hiding in a round that runs once per outer iteration)
-// Jm: J (D×D) from where the caller keeps it (default P.J) — inside the optimiser loop an LDS copy, whose
-// reads are not hoisted: the D² fp64 conversions of P.J hoisted out of the round loop held 2·D² VGPRs
-template <int D, int U = 8>
+// JL: J (D×D) from Jm, an LDS copy (inside the optimiser loop, whose reads are not hoisted: the D² fp64
+// conversions of P.J hoisted out of the round loop held 2·D² VGPRs), else from P.J.  A compile-time
+// choice: a run-time select between &P.J and an LDS address takes the kernel argument's address, and the
+// compiler then copies all of KParams into scratch and reads every parameter from there (1.8 KB of
+// scratch and ≈60 scratch loads in the dual-loop / BLS rounds, round 4)
+template <int D, int U = 8, bool JL = false>
 __device__ void eval_exact(const KParams& P, const float* __restrict__ Xa, int n, float (&q)[D], float (&v)[D],
                            const float* Kt = nullptr, const float* dKt = nullptr, int rs = kLd, int cs = 1,
                            const float* Jm = nullptr) {
-    const float* J = Jm ? Jm : P.J;
+    const float* J;
+    if constexpr (JL) J = Jm;
+    else J = P.J;
     const int N = P.N;
     double aq[D], av[D];
 #pragma unroll
@@ -2988,7 +2993,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
                 for (int j = 0; j < WPL; ++j) {
                     if (vl[j]) {
-                        if constexpr (D <= 3) eval_exact<D, kResyncU>(P, X + (t * D) * ldx, nn[j], q[j], v[j], nullptr, nullptr, 1, ldx, Jl);
+                        if constexpr (D <= 3) eval_exact<D, kResyncU, true>(P, X + (t * D) * ldx, nn[j], q[j], v[j], nullptr, nullptr, 1, ldx, Jl);
                         else eval_exact_loop<D, 4>(P, X + (t * D) * ldx, ldx, nn[j], N, Jl, q[j], v[j]);
                         // the last extended-vis frame shows the exact trajectory of the returned α
                         if (rec && st.series_len > 0) {
