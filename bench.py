@@ -193,11 +193,31 @@ def cpu_baseline_batched(args, start, goal, obstacles, cores, budget_s=10.0):
                       f"1-core rate {rate1:.1f} it/s"}
 
 
-def cpu_baseline(cfg, args, start, goal, obstacles):
+# CPU-baseline budgets (seconds of timed CPU work: scalar oracle, batched numpy).  At world > 1 the other
+# ranks wait in the rendezvous while rank 0 times them, so they are capped there (CPU_BUDGET_MULTI_S)
+# and init_process_group's timeout is set explicitly to cover the wait (rendezvous_timeout).
+CPU_BUDGET_S = (12.0, 10.0)
+CPU_BUDGET_MULTI_S = (4.0, 3.0)
+
+
+def cpu_budgets(world):
+    return CPU_BUDGET_S if world <= 1 else CPU_BUDGET_MULTI_S
+
+
+def rendezvous_timeout(world):
+    """init_process_group's timeout: rank 0's capped CPU-baseline work (measured sample ≈ budget, plus the
+    1-thread calibration runs and the worker pool's start-up) with a wide margin — bounded, not the
+    backend's default."""
+    import datetime
+    return datetime.timedelta(seconds=int(120 + 10 * sum(cpu_budgets(world))))
+
+
+def cpu_baseline(cfg, args, start, goal, obstacles, world=1):
     """Both CPU restatements timed on this host (rank 0's shard); `value` is the faster one."""
     cores = max(1, min(16, len(os.sched_getaffinity(0))))
-    port = cpu_baseline_port(args, start, goal, obstacles, cores)
-    batched = cpu_baseline_batched(args, start, goal, obstacles, cores)
+    b_port, b_batched = cpu_budgets(world)
+    port = cpu_baseline_port(args, start, goal, obstacles, cores, budget_s=b_port)
+    batched = cpu_baseline_batched(args, start, goal, obstacles, cores, budget_s=b_batched)
     best = port if batched is None or port["value"] >= batched["value"] else batched
     return {"value": best["value"], "unit": ("GD" if args.optimizer_name == "gd" else "BLS") + " iterations/s",
             "cores": cores, "kind": "port", "sample": best["label"] + ": " + best["sample"],
@@ -321,6 +341,12 @@ def dry_run(a, world, rank):
     shards = [torch.zeros_like(shard) for _ in range(world)] if world > 1 else [shard]
     if world > 1:
         dist.all_gather(shards, shard)
+    # the global-batch rows this rank's shard holds (make_problem's slice), gathered in rank order
+    rng = torch.tensor([rank * B, (rank + 1) * B], dtype=torch.int64)
+    ranges = [torch.zeros_like(rng) for _ in range(world)] if world > 1 else [rng]
+    if world > 1:
+        dist.all_gather(ranges, rng)
+    world_seen = dist.get_world_size() if world > 1 else 1
     if rank == 0:
         print(json.dumps({"metric": ("GD" if opt == "gd" else "BLS") + " iterations/sec (batch of trajectories)",
                           "value": None, "dry_run": True,
@@ -328,7 +354,10 @@ def dry_run(a, world, rank):
                           "config": config_record(a, args, desc, B, N, D, O, opt, world, None),
                           "obstacles_equal_rank0": bool(same.item() == 1.0),
                           "elapsed_max": elapsed_max, "iterations_all": iters_all,
-                          "shard_checksums": [float(x.item()) for x in shards]}), flush=True)
+                          "shard_checksums": [float(x.item()) for x in shards],
+                          "shard_ranges": [[int(v) for v in x.tolist()] for x in ranges],
+                          "world_size": world_seen,
+                          "rendezvous_timeout_s": rendezvous_timeout(world).total_seconds()}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -375,12 +404,13 @@ def main():
     # The other ranks wait for rank 0 in the rendezvous meanwhile.
     cpu = None
     if rank == 0 and not a.no_cpu_baseline and not a.dry_run:
-        cpu = cpu_baseline(a.config, args, start, goal, obstacles)
+        cpu = cpu_baseline(a.config, args, start, goal, obstacles, world)
     if world > 1:
+        tmo = rendezvous_timeout(world)
         if gloo or a.dry_run:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=tmo)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
     if a.dry_run:
         return dry_run(a, world, rank)
 

@@ -123,12 +123,15 @@ def build(force=False, verbose=False, variant="", jobs=None):
     os.makedirs(odir, exist_ok=True)
     jobs = jobs or min(16, os.cpu_count() or 1)
     todo, objs = [], []
-    stamp = os.path.join(odir, "flags.txt")  # a change of flags rebuilds every object
+    # a change of flags rebuilds every object; the stamp is written only after every object compiled and
+    # the link succeeded (and removed when a compile fails), so a build interrupted after a flag change
+    # cannot leave objects of the old flags looking current
+    stamp = os.path.join(odir, "flags.txt")
     flagtxt = "\n".join(CFLAGS + extra)
     if not os.path.exists(stamp) or open(stamp).read() != flagtxt:
         force = True
-        with open(stamp, "w") as fh:
-            fh.write(flagtxt)
+        if os.path.exists(stamp):
+            os.remove(stamp)
     for oname, src, flags in units(variant):
         obj = os.path.join(odir, oname + ".o")
         objs.append(obj)
@@ -156,11 +159,18 @@ def build(force=False, verbose=False, variant="", jobs=None):
                 i += 1
             return out
         todo = [drop_sched(cmd) for cmd in todo]
-    if todo:
-        with ThreadPoolExecutor(jobs) as ex:
-            list(ex.map(run, todo))
-    if todo or force or _newer(out, objs):
-        run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs)
+    try:
+        if todo:
+            with ThreadPoolExecutor(jobs) as ex:
+                list(ex.map(run, todo))
+        if todo or force or _newer(out, objs):
+            run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs)
+    except BaseException:
+        if os.path.exists(stamp):
+            os.remove(stamp)
+        raise
+    with open(stamp, "w") as fh:
+        fh.write(flagtxt)
     return out
 
 

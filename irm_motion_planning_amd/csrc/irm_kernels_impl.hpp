@@ -2845,6 +2845,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     // the neighbouring slot: the other SIMD pair (slot s = waves 2s, 2s+1 → SIMDs 2s mod 4,
                     // 2s+1 mod 4 at two waves per slot), so the helper's VALU does not share t*'s SIMDs
                     hs = ts ^ 1;
+                    // the helper's MFMA columns must exist: with five 3-joint trajectories per workgroup
+                    // (N ≤ 64, traj_per_block = 5) slot 5 would own columns 15-17 — take the slot below t*
+                    // then (ts ≥ 2 there, and slot ts − 1's columns end below t*'s)
+                    if ((hs + 1) * D > kCols) hs = ts - 1;
                     helper = t == hs;
                 }
             }
@@ -3492,8 +3496,10 @@ inline int lean_flow(const KParams& p) {
     if (p.optimizer == IRM_OPT_BLS) return LF_BLS;
     return (p.max_outer <= 1 && !p.record_series) ? LF_GD1 : LF_GD2;
 }
-inline bool lean_fits(const KParams& p) {
-    return (p.RP / 16) * p.nsplit <= p.BT / 64 && p.NK / 16 <= 4 * p.nsplit && lean_lds(p) <= 160 * 1024;
+// help: the launch's instantiation carries the BLS line-search helpers' exchange regions (lean_help), so
+// the check sees the LDS the launch will request (per-problem obstacle tables grow the base with TB·O)
+inline bool lean_fits(const KParams& p, bool help = false) {
+    return (p.RP / 16) * p.nsplit <= p.BT / 64 && p.NK / 16 <= 4 * p.nsplit && lean_lds(p, help) <= 160 * 1024;
 }
 
 // k_optimize<Shape> with the MAXT / operator-placement / optimiser variants (one shape per
@@ -3572,7 +3578,8 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s, LaunchDesc* de
         }
         if constexpr (!Sh::kVariants && TT <= 512) {  // the lean kernel (F operators register-resident:
             // one stage-1 unit per wave; workgroups are padded to TT threads by choose_shape)
-            if (flow >= 0 && p.BT == TT && lean_fits(p)) return launch_lean_flow<Sh, TT, 1, true>(p, flow, grid, s, desc);
+            const bool help = flow == LF_BLS && lean_help<Sh, TT, 1, true, LF_BLS>();
+            if (flow >= 0 && p.BT == TT && lean_fits(p, help)) return launch_lean_flow<Sh, TT, 1, true>(p, flow, grid, s, desc);
         }
         if constexpr (!Sh::kVariants && TT == 1024) {
             if constexpr (Sh::kNW == 256 && Sh::D * 3 <= kCols) {  // ≥ 3 trajectories fit the MFMA columns

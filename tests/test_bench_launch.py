@@ -95,3 +95,28 @@ def test_cpu_baseline_runs_before_process_group_init(monkeypatch):
     except Stop:
         pass
     assert order == ["cpu_baseline", "init_process_group"], order
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("cfg,global_batch", [("c4", 8192), ("c5", 4096)])
+def test_eight_rank_dry_run_shards_cover_the_global_batch(cfg, global_batch):
+    """BASELINE configs[3] / [4] as the driver's 8-GPU run launches them (--gpus 8, one rank per GPU):
+    eight disjoint shards, in rank order, covering the global batch exactly; the collectives ran over
+    eight ranks; the rendezvous timeout is explicit and covers rank 0's capped CPU-baseline budget
+    (VERDICT r04 #6)."""
+    sys.path.insert(0, REPO)
+    import bench
+    r = _bench("--gpus", "8", "--dry-run", "--config", cfg)
+    assert r["n_gpus"] == 8 and r["world_size"] == 8
+    assert r["config"]["global_batch"] == global_batch
+    B = r["config"]["batch_per_gpu"]
+    assert B * 8 == global_batch
+    ranges = r["shard_ranges"]
+    assert ranges == [[k * B, (k + 1) * B] for k in range(8)]  # disjoint, contiguous, in rank order
+    assert len(set(r["shard_checksums"])) == 8
+    assert r["obstacles_equal_rank0"]
+    assert r["elapsed_max"] == 8.0 and r["iterations_all"] == global_batch * 200
+    assert bench.cpu_budgets(8) < bench.cpu_budgets(1)
+    assert r["rendezvous_timeout_s"] >= 10 * sum(bench.cpu_budgets(8))
