@@ -235,16 +235,24 @@ __host__ __device__ inline Plan plan_lds(const KParams& p, bool ops_lds, bool op
 // the stage-1 splits where the LDS allows (vlds shapes: N ≤ 128, D ≤ 3), so the units stay one per wave
 __host__ __device__ constexpr int lean_zsplit(int nsplit, bool vlds) { return vlds ? 2 * nsplit : nsplit; }
 struct LeanX {
-    int vt, vn, eb, zp, gb, ep, ep0, ss, hp, total;
+    int vt, vn, eb, zp, gb, ep, ep0, ss, hp, aj, ts, total;
 };
+// BLS flow of k_lean: the trial's residual projection z = V_Rᵀ·e' is formed by the G-tile waves, one
+// partial per wave, stored quad-major (partial w, row quad rq, column c at w·256 + rq·64 + c·4: a lane's
+// f32x4 of an MFMA tile — b128 stores and B-operand reads conflict-free); at most 8 waves (MAXT ≤ 512)
+__host__ __device__ constexpr int lean_bls_nzp(int NK) { return NK / 16 < 8 ? NK / 16 : 8; }
+// per-slot trial scalars of the BLS flow (TS): lr, ‖G‖, "in a line search" flag, spare
+constexpr int kTsW = 4;
 // compact copy of each trajectory's endpoint velocity rows b'[0], b'[N−1] of X (k_lean): kEpS floats each
 constexpr int kEpS = 8;
 __host__ __device__ constexpr int lean_ld(int NK) { return NK + 8; }
 // help_threads > 0: the BLS line-search helpers' exchange regions (k_lean, kHelp): a trajectory's α, T, V
 // rows by thread ([3·D][threads], ss) and its per-round scalars (8 words per trajectory slot, hp)
 constexpr int kHpW = 8;
+// bls: the BLS flow's regions — α rows (Ab, in e.eb's place), the trial iterate's rows (Aj), the z partials
+// (quad-major, lean_bls_nzp) and the per-slot trial scalars (TS) instead of the GD flows' e' / z regions
 __host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, int nsplit, bool vlds, int D = 0,
-                                            int help_threads = 0) {
+                                            int help_threads = 0, bool bls = false) {
     LeanX e{};
     int off = base;
     e.vt = e.vn = 0;
@@ -256,8 +264,18 @@ __host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, in
     }
     e.eb = off;
     off += al4(16 * lean_ld(NK));
-    e.zp = off;
-    off += al4(lean_zsplit(nsplit, vlds) * 16 * lean_ldy(RP));
+    e.aj = e.ts = 0;
+    if (bls) {
+        e.aj = off;
+        off += al4(16 * lean_ld(NK));
+        e.zp = off;
+        off += lean_bls_nzp(NK) * 256;
+        e.ts = off;
+        off += kMaxTraj * kTsW;
+    } else {
+        e.zp = off;
+        off += al4(lean_zsplit(nsplit, vlds) * 16 * lean_ldy(RP));
+    }
     e.gb = off;
     off += al4(16 * lean_ld(NK));
     e.ep = off;

@@ -909,6 +909,19 @@ __device__ __forceinline__ float unfused(float x) {
     return x;
 }
 
+// a/b through a reciprocal refined by one Newton step (r = rcp_refined(b)): q = a·r, then q + (a − q·b)·r —
+// the correctly rounded quotient but in rare near-ties, in 3 VALU per quotient once r is known (the IEEE
+// division expands to ~10 with its scaling and fix-up).  The BLS trial stages form ĝ = G/‖G‖ with it
+// (optimizer_BLS.py:165); its operands are normal numbers there.
+__device__ __forceinline__ float rcp_refined(float b) {
+    const float r0 = __builtin_amdgcn_rcpf(b);
+    return fmaf(fmaf(-b, r0, 1.f), r0, r0);
+}
+__device__ __forceinline__ float div_rcp(float a, float b, float r) {
+    const float q = a * r;
+    return fmaf(fmaf(-q, b, a), r, q);
+}
+
 // Smallest step a rounding residual is folded with (e' = −e/step): |e'| ≤ 1e-3·2^80 ≈ 1e21 stays
 // finite where a tiny BLS step (lr/‖G‖ after many rejected trials, or --gd-lr 0) would give ±inf.
 constexpr float kMinRefStep = 8.271806e-25f;  // 2^-80
@@ -2047,7 +2060,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     float* obsL = smem + H.obs;
     const int nsplit = sh.NSPLIT, zsplit = lean_zsplit(sh.NSPLIT, VL);
     constexpr bool kHelp = lean_help<S, MAXT, WPL, FULL, FLOW>();
-    const LeanX LX = lean_extra(plan_lds(P, false, true, true).total, MP, NK, RP, nsplit, VL, D, kHelp ? MAXT : 0);
+    const LeanX LX = lean_extra(plan_lds(P, false, true, true).total, MP, NK, RP, nsplit, VL, D, kHelp ? MAXT : 0, BLS);
     float* Eb = smem + LX.eb;  // e' rows [column][waypoint]
     float* Zp = smem + LX.zp;  // stage-1 partials of V_Rᵀ·e'
     float* Gb = smem + LX.gb;  // (V_R·y'')[waypoint] rows [column][waypoint]
@@ -2120,7 +2133,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             ln[e] = gn[e];
         }
     }
-    for (int e = tid; e < 16 * lde; e += P.BT) Eb[e] = 0.f;  // no pending residual; rows ≥ N stay 0
+    for (int e = tid; e < 16 * lde; e += P.BT) Eb[e] = 0.f;  // no pending residual; rows ≥ N stay 0 (BLS: α rows)
+    if constexpr (BLS)
+        for (int e = tid; e < kMaxTraj * kTsW; e += P.BT) smem[LX.ts + e] = 0.f;  // no slot in a line search yet
     for (int e = tid; e < kMaxTraj * 2 * kEpS + 4; e += P.BT) smem[LX.ep + e] = 0.f;  // + the zero word
     stage_obstacles(P, tb0, ntb, obsL);
     stage_alpha<D>(P, tb0, ntb, X, NK);
@@ -2152,6 +2167,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         for (int k = 0; k < D; ++k) {
             q[j][k] = v[j][k] = 0.f;
             al[j][k] = vl[j] ? X[nn[j] * kLd + t * D + k] : 0.f;
+            // BLS: the α rows the trial stages read (written with every accepted trial)
+            if (BLS && vl[j]) Eb[(t * D + k) * lde + swz(nn[j], t * D + k)] = al[j][k];
         }
         if (vl[j]) {
             eval_exact<D>(P, X + t * D, nn[j], q[j], v[j]);
@@ -2649,6 +2666,227 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4x) = ag;
         }
     };
+    // ---- BLS trial stages.  A trial j of a line search is evaluated at its own fp32 iterate
+    // α_j = fl(fl(c_j·α) − fl(lr_j·ĝ)) (optimizer_BLS.py:139-140): its trajectory is c_j·[T; V] − s_j·F·(y'' + z_j)·J
+    // with z_j = V_Rᵀ·e'_j, e'_j = −(α_j − (c_j·α − s_j·G))/s_j the iterate's rounding residual.
+    // The G-tile waves form e'_j themselves, element by element of their G tiles (the MFMA result layout
+    // of a tile is the k-permuted B layout of the z MFMAs over the same 16 waypoints), and accumulate their
+    // tiles' share of z_j in the same pass: no per-lane residual rows, no barrier between G, the residual
+    // and z.  A round with a new direction: stage 1 → barrier → G tiles + ‖G‖ + α_j + z partials →
+    // barrier → F tiles → barrier; a round that continues a line search: α_j + z partials from the stored
+    // G / α rows → barrier → F tiles → barrier.  Every column's trial is its trajectory's current one (lr
+    // from TS); a helper's columns take t*'s next (lr·β₋): ycl is the column whose y'', G and α the
+    // lane's column reads.
+    constexpr int kNZP = lean_bls_nzp(S::kNW > 0 ? S::NK : 256);
+    const int nzp = min(nwaves, MTG);  // z partials (one per G-tile wave)
+    constexpr bool kBFix = FULL && S::kNW > 0;
+    constexpr int kNZc = kBFix ? (MAXT / 64 < S::NK / 16 ? MAXT / 64 : S::NK / 16) : 1;
+    static_assert(!BLS || !kBFix || kNZc <= kNZP, "z partials fit their region");
+    float* Ab = smem + LX.eb;    // BLS: α rows [column][waypoint] (Eb's place)
+    float* Ajb = smem + LX.aj;   // BLS: the round's trial iterate α_j, rows [column][waypoint]
+    float* Zq = smem + LX.zp;    // BLS: z partials, quad-major
+    float* TS = smem + LX.ts;    // BLS: per-slot lr, ‖G‖, in-a-line-search flag
+    auto bls_gz = [&](auto freshc, bool hmr, int hsr) {  // fresh (a new direction this round): G from y''
+        constexpr bool fresh = decltype(freshc)::value;
+        const int pz = nwaves - 1 - wave;  // this wave's z partial; its G tiles are u = pz + g·nwaves
+        if (pz >= MTG) return;             // (wave-uniform)
+        const int sc = ycl / D;            // the trial's trajectory slot (t* for a helper's columns)
+        // the slot's trial scalars, read with the round's first LDS batch
+        const float lrs = TS[sc * kTsW + 0];
+        const bool act = TS[sc * kTsW + 2] != 0.f;  // (other slots: no residual)
+        constexpr int kT = kBFix ? (S::NK / 16 + MAXT / 64 - 1) / (MAXT / 64) : 1;  // tiles per wave (fixed)
+        const int ntl = kBFix ? kT : (MTG - pz + nwaves - 1) / nwaves;
+        f32x4 Gt[kBFix ? kT : 1];
+        // fixed shapes: every tile's α rows and V_Rᵀ fragment (and, continuing a search, its stored G) read
+        // in the round's first LDS batch
+        f32x4 Ap[kBFix ? kT : 1], Vp[kBFix ? kT : 1];
+        if constexpr (kBFix) {
+#pragma unroll
+            for (int g = 0; g < kT; ++g) {
+                const int u = pz + g * (MAXT / 64);
+                Ap[g] = Vp[g] = Gt[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (u < S::NK / 16) {
+                    Ap[g] = *reinterpret_cast<const f32x4*>(Ab + ycl * lde + u * 16 + r4y);
+                    Vp[g] = reinterpret_cast<const f32x4*>(VT)[(size_t)u * 64 + lane];
+                    if constexpr (!fresh) Gt[g] = *reinterpret_cast<const f32x4*>(Gb + ycl * lde + u * 16 + r4y);
+                }
+            }
+        }
+        float gn;
+        if constexpr (fresh) {
+            // y'' of column ycl, ranks r4..r4+3 and 16+r4..19+r4, summed over the stage-1 splits in order
+            f32x4 y0, y1;
+            if constexpr (kBFix) {
+                f32x4 yp[S::NSPLIT], yq[S::NSPLIT], gv[kT][2];
+#pragma unroll
+                for (int sp = 0; sp < S::NSPLIT; ++sp) {
+                    yp[sp] = *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + ycl) * ldy + r4y);
+                    yq[sp] = *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + ycl) * ldy + 16 + r4y);
+                }
+#pragma unroll
+                for (int g = 0; g < kT; ++g) {
+                    const f32x4* ap = reinterpret_cast<const f32x4*>(VN) + (size_t)(pz + g * (MAXT / 64)) * KQ2 * 64 + lane;
+                    gv[g][0] = gv[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    if (pz + g * (MAXT / 64) < S::NK / 16) {
+                        gv[g][0] = ap[0];
+                        gv[g][1] = ap[64];
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                y0 = yp[0];
+                y1 = yq[0];
+#pragma unroll
+                for (int sp = 1; sp < S::NSPLIT; ++sp) {
+                    y0 += yp[sp];
+                    y1 += yq[sp];
+                }
+                // G = V_R·y'' at rank 24 (kR24, the order of stage2f), issued before the norm's VALU work
+#pragma unroll
+                for (int g = 0; g < kT; ++g) {
+                    Gt[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    if (pz + g * (MAXT / 64) < S::NK / 16) {
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) Gt[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[g][0][m], y0[m], Gt[g], 0, 0, 0);
+#pragma unroll
+                        for (int m = 0; m < 2; ++m) Gt[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(gv[g][1][m], y1[m], Gt[g], 0, 0, 0);
+                    }
+                }
+            } else {
+                y0 = *reinterpret_cast<const f32x4*>(Ypart + ycl * ldy + r4y);
+                y1 = *reinterpret_cast<const f32x4*>(Ypart + ycl * ldy + 16 + r4y);
+                for (int sp = 1; sp < nsplit; ++sp) {
+                    y0 += *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + ycl) * ldy + r4y);
+                    y1 += *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + ycl) * ldy + 16 + r4y);
+                }
+            }
+            // ‖G‖² = ‖y''‖² (V_R orthonormal) per trajectory (optimizer_BLS.py:165): the lane's 8 squares, the
+            // column over its four lane rows (permlane swaps: the same sums in the same order in every lane),
+            // then the slot's D columns in column order (lanes sc·D + a of row 0); every G-tile wave forms
+            // the same values
+            float sq = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sq = fmaf(y0[i], y0[i], sq);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) sq = fmaf(y1[i], y1[i], sq);
+            const auto p16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(sq), __float_as_uint(sq), false, false);
+            const float s2 = __uint_as_float(p16[0]) + __uint_as_float(p16[1]);
+            const auto p32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(s2), __float_as_uint(s2), false, false);
+            const int cs = __float_as_int(__uint_as_float(p32[0]) + __uint_as_float(p32[1]));
+            float g2 = __int_as_float(__builtin_amdgcn_ds_bpermute((sc * D) << 2, cs));
+#pragma unroll
+            for (int a = 1; a < D; ++a) g2 += __int_as_float(__builtin_amdgcn_ds_bpermute((sc * D + a) << 2, cs));
+            gn = __builtin_amdgcn_sqrtf(g2);  // v_sqrt_f32 (≤ 1 ulp): every user reads this value (TS)
+            if (pz == 0 && lane < kCols && ycl == cl && cl % D == 0) TS[(cl / D) * kTsW + 1] = gn;  // for the trajectories and the later rounds
+            if constexpr (!kBFix) {
+                const f32x4* ap = reinterpret_cast<const f32x4*>(VN) + (size_t)pz * KQ2 * 64 + lane;
+                const f32x4 g0 = ap[0], g1 = ap[64];
+                Gt[0] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int m = 0; m < 4; ++m) Gt[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(g0[m], y0[m], Gt[0], 0, 0, 0);
+#pragma unroll
+                for (int m = 0; m < 2; ++m) Gt[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(g1[m], y1[m], Gt[0], 0, 0, 0);
+                (void)ntl;
+            }
+        } else {
+            gn = TS[sc * kTsW + 1];
+        }
+        const float lrx = (hmr && cl / D == hsr) ? lrs * P.bls_bm : lrs;  // a helper: t*'s next trial (:147)
+        const float cjx = unfused(1.f - unfused(P.lreg * lrx));            // optimizer_BLS.py:139
+        // ĝ = G/‖G‖ (optimizer_BLS.py:165) and the step lr/‖G‖ through one refined reciprocal (div_rcp)
+        const float rg = rcp_refined(gn);
+        const float sx = div_rcp(lrx, gn, rg);  // the trajectory lanes' step (the same expression there)
+        const float ne = -rcp_refined(fmaxf(sx, kMinRefStep));
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        auto tile = [&](int u, f32x4 G, bool store_g, f32x4 A, f32x4 a) {  // α rows, V_Rᵀ fragment (rank tile 0)
+            if (store_g) *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4x) = G;  // for the later rounds
+            f32x4 AJ, E;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float gh = div_rcp(G[i], gn, rg);
+                // α_j = fl(fl(c·α) − fl(lr·ĝ)) (optimizer_BLS.py:139) and its scaled residual e' = (c·α − α_j)/s − G,
+                // u = fl(c·α − α_j) in one rounding (alpha_step_gd2's form: e' to 2^-24 of |G|)
+                const float p1 = unfused(cjx * A[i]), p2 = unfused(lrx * gh);
+                AJ[i] = unfused(p1 - p2);
+                const float uu = fmaf(cjx, A[i], -AJ[i]);
+                E[i] = act ? fmaf(-uu, ne, -G[i]) : 0.f;
+            }
+            *reinterpret_cast<f32x4*>(Ajb + cl * lde + u * 16 + r4x) = AJ;
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], E[0], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], E[1], acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], E[2], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], E[3], acc1, 0, 0, 0);
+        };
+        if constexpr (kBFix) {
+#pragma unroll
+            for (int g = 0; g < kT; ++g) {
+                const int u = pz + g * (MAXT / 64);
+                if (u < S::NK / 16) tile(u, Gt[g], fresh, Ap[g], Vp[g]);
+            }
+        } else {
+            for (int u = pz; u < MTG; u += nwaves) {
+                f32x4 G;
+                if (fresh && u == pz) {
+                    G = Gt[0];
+                } else if (fresh) {  // further tiles of the wave (general launches)
+                    const f32x4* ap = reinterpret_cast<const f32x4*>(VN) + (size_t)u * KQ2 * 64 + lane;
+                    const f32x4 g0 = ap[0], g1 = ap[64];
+                    f32x4 y0 = *reinterpret_cast<const f32x4*>(Ypart + ycl * ldy + r4y);
+                    f32x4 y1 = *reinterpret_cast<const f32x4*>(Ypart + ycl * ldy + 16 + r4y);
+                    for (int sp = 1; sp < nsplit; ++sp) {
+                        y0 += *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + ycl) * ldy + r4y);
+                        y1 += *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + ycl) * ldy + 16 + r4y);
+                    }
+                    G = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int m = 0; m < 4; ++m) G = __builtin_amdgcn_mfma_f32_16x16x4f32(g0[m], y0[m], G, 0, 0, 0);
+#pragma unroll
+                    for (int m = 0; m < 2; ++m) G = __builtin_amdgcn_mfma_f32_16x16x4f32(g1[m], y1[m], G, 0, 0, 0);
+                } else {
+                    G = *reinterpret_cast<const f32x4*>(Gb + ycl * lde + u * 16 + r4y);
+                }
+                tile(u, G, fresh, *reinterpret_cast<const f32x4*>(Ab + ycl * lde + u * 16 + r4y),
+                     reinterpret_cast<const f32x4*>(VT)[(size_t)u * 64 + lane]);
+            }
+        }
+        *reinterpret_cast<f32x4*>(Zq + pz * 256 + (r4 >> 2) * 64 + cl * 4) = acc0 + acc1;
+    };
+    // the F tiles of every column's trial: dP = F·(y'' + Σ_w z partial w) at rank 16 (kR16F)
+    auto bls_f = [&]() {
+        const float* zq = Zq + (r4 >> 2) * 64 + cl * 4;
+        f32x4 by0, bz;
+        if constexpr (kBFix) {  // every partial read before the first sum (one LDS round trip)
+            f32x4 yp[S::NSPLIT], zz[kNZc];
+#pragma unroll
+            for (int sp = 0; sp < S::NSPLIT; ++sp) yp[sp] = *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + ycl) * ldy + r4y);
+#pragma unroll
+            for (int w = 0; w < kNZc; ++w) zz[w] = *reinterpret_cast<const f32x4*>(zq + w * 256);
+            __builtin_amdgcn_sched_barrier(0);
+            by0 = yp[0];
+#pragma unroll
+            for (int sp = 1; sp < S::NSPLIT; ++sp) by0 += yp[sp];
+            bz = zz[0];
+#pragma unroll
+            for (int w = 1; w < kNZc; ++w) bz += zz[w];
+        } else {
+            by0 = *reinterpret_cast<const f32x4*>(Ypart + ycl * ldy + r4y);
+            for (int sp = 1; sp < nsplit; ++sp) by0 += *reinterpret_cast<const f32x4*>(Ypart + (sp * 16 + ycl) * ldy + r4y);
+            bz = *reinterpret_cast<const f32x4*>(zq);
+            for (int w = 1; w < nzp; ++w) bz += *reinterpret_cast<const f32x4*>(zq + w * 256);
+        }
+        const f32x4 bt = by0 + bz;
+        f32x4 acc[S2T];
+#pragma unroll
+        for (int j = 0; j < S2T; ++j) {
+            acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (wave + j * nwaves < MT2) {
+#pragma unroll
+                for (int m = 0; m < 4; ++m) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2][m], bt[m], acc[j], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < S2T; ++j)
+            if (wave + j * nwaves < MT2) *reinterpret_cast<f32x4*>(dP + cl * ldx + (wave + j * nwaves) * 16 + r4x) = acc[j];
+    };
     // this lane's direction rows Δ = (F·y'')·J for waypoint j (the endpoint velocity rows are in y'')
     auto direction = [&](int j, float (&dt)[D], float (&dv)[D]) {
         float ut[D], uv[D];
@@ -2719,10 +2957,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         }
     };
     bool adopt = false;  // t*: the helper's trial was accepted — take its α, T, V at the next round's start
-    float aj[BLS ? WPL : 1][D];  // BLS: the trial's fp32 iterate α_j
-#pragma unroll
-    for (int k = 0; k < D; ++k) aj[0][k] = 0.f;
-    bool pre_eb = false;  // BLS: this trajectory's next trial iterate and residual are formed already
+    // BLS: this trajectory's trial scalars for the trial stages (lr of its next trial, in a line search)
+    auto ts_write = [&]() {
+        if (n0 == 0 && lane == 0) {
+            TS[t * kTsW + 0] = lr;
+            TS[t * kTsW + 2] = phase == LP_STEP ? 1.f : 0.f;
+        }
+    };
     int n_rounds = 0, n_hm = 0;  // diagnostics (trace_b bit 29): kernel rounds / helper rounds until this trajectory ended
 
     // round 0 (optimizer_GD.py:93 / :210: the loss at α0) and the first gradient inputs
@@ -2768,6 +3009,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             bfar = grad_inputs(w, q, v, f.idx, lsg, ljl, t);
             xdense = bfar;
         }
+        if constexpr (BLS) {
+            if (tvalid) ts_write();
+        }
         if constexpr (kHelp) {
             if (tvalid) {
                 ss_write(t, al, q, v);
@@ -2786,7 +3030,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         } else {
             if (lane == 0 && tvalid)
                 atomicOr(&fw[0], (1u << wave) | (needs_dir ? 1u << 28 : 0u) | (phase == LP_RESYNC ? 1u << 29 : 0u) |
-                                     (phase == LP_STEP ? (BLS ? (1u << 30) | (1u << 27) : 1u << 30) : 0u) |
+                                     (phase == LP_STEP ? 1u << 30 : 0u) |
                                      ((BLS ? xdense && phase == LP_STEP : bfar) ? 1u << 31 : 0u));
         }
     }
@@ -2810,7 +3054,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
     for (int par = 0;; par ^= 1) {
         f32x4 pre1[KQU1], pre1w[KQU1];
-        float pre1e;  // read only on the endpoint waves (hasep)
+        float pre1e = 0.f;  // read only on the endpoint waves (hasep)
         if constexpr (kPre1) stage1_load(pre1, pre1w, pre1e);
         const unsigned fl = fw[par];
         if constexpr (GD1) {
@@ -2873,47 +3117,60 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             }
         }
         IRM_STAMP(0);
-        if (dirr) {  // block-uniform
-            IRM_COUNT(13, dense);
-            stage1(dense, pre1, pre1w, pre1e);
-            if constexpr (!BLS) stage1z();  // (BLS: the trials' residuals have their own stage below)
-            IRM_STAMP(1);
-            __syncthreads();
-            IRM_STAMP(2);
-            if constexpr (BLS) {
-                // ‖G‖² = ‖y''‖², alpha_norm·‖G‖ = Σ_r (y''_r·1)² with G = V_R·y'' (optimizer_BLS.py:165-166
-                // without forming G; the endpoint velocity rows are in y''), rows r = li < RP of the
-                // trajectory's first wave
+        if constexpr (!BLS) {
+            if (dirr) {  // block-uniform
+                IRM_COUNT(13, dense);
+                stage1(dense, pre1, pre1w, pre1e);
+                stage1z();
+                IRM_STAMP(1);
+                __syncthreads();
+                IRM_STAMP(2);
+                stage2f(std::true_type{}, std::true_type{});
+                IRM_STAMP(3);
+                __syncthreads();
+                IRM_STAMP(4);
+            }
+        } else if ((fl >> 30) & 1u) {  // block-uniform: some trajectory has a line-search trial this round
+            // (a round with a new direction: stage 1 first; the trial stages of bls_gz / bls_f, above)
+            if (dirr) {
+                IRM_COUNT(13, dense);
+                stage1(dense, pre1, pre1w, pre1e);
+                IRM_STAMP(1);
+                __syncthreads();
+                IRM_STAMP(2);
+            }
+            if (dirr) bls_gz(std::true_type{}, hm, hs);
+            else bls_gz(std::false_type{}, hm, hs);
+            if (dirr) {
+                // alpha_norm·‖G‖ = Σ_r (y''_r·1)² with G = V_R·y'' (optimizer_BLS.py:166 without forming G; the
+                // endpoint velocity rows are in y''), rows r = li < RP of the trajectory's first wave (‖G‖:
+                // the G-tile waves, bls_gz)
                 if (needs_dir && n0 == 0) {  // wave-uniform
-                    float g2 = 0.f, s1 = 0.f;
+                    float s1 = 0.f;
                     if (tvalid && li < RP) {
                         float sa = 0.f;
 #pragma unroll
                         for (int a = 0; a < D; ++a) {
                             float y = Ypart[(t * D + a) * ldy + swz(li, t * D + a)];
                             for (int sp = 1; sp < nsplit; ++sp) y += Ypart[(sp * 16 + t * D + a) * ldy + swz(li, t * D + a)];
-                            g2 = fmaf(y, y, g2);
                             sa += y;
                         }
                         s1 = sa * sa;
                     }
-                    g2 = wred_sum(g2);
                     s1 = wred_sum(s1);
-                    if (lane == 0) {
-                        wp[t * 2] = g2;
-                        wp[t * 2 + 1] = s1;
-                    }
+                    if (lane == 0) wp[t * 2 + 1] = s1;
                 }
             }
-            stage2f(std::bool_constant<!BLS>{}, std::true_type{});  // (BLS: G only; F below, per trial)
             IRM_STAMP(3);
             __syncthreads();
             IRM_STAMP(4);
+            bls_f();
+            __syncthreads();
         }
         // ------------------------------------------------ BLS: a new direction (the inner-loop head)
         if constexpr (BLS) {
             if (needs_dir) {  // wave-uniform; optimizer_BLS.py:163-166
-                gnorm = sqrtf(wp[t * 2]);
+                gnorm = TS[t * kTsW + 1];  // ‖G‖ as the trial stages used it (bls_gz)
                 anorm = wp[t * 2 + 1] / gnorm;
                 st.grad_evals++;  // cost + grad at α (optimizer_BLS.py:163-164)
                 st.cost_evals++;
@@ -2925,57 +3182,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         float cj = cfac, stepj = lr, lrj = lr, gnj = gnorm;
         if constexpr (BLS) {
             if (helper) {
-                h_gn = sqrtf(wp[ts * 2]);  // t*'s ‖G‖ and alpha_norm, the same expressions as t*'s latch
+                h_gn = TS[ts * kTsW + 1];  // t*'s ‖G‖ and alpha_norm, the same values as t*'s latch
                 h_an = wp[ts * 2 + 1] / h_gn;
                 lrj = h_lr;
                 gnj = h_gn;
             }
             cj = unfused(1.f - unfused(P.lreg * lrj));  // (1 − λ_reg·bls_lr) in fp32 (optimizer_BLS.py:139)
-            stepj = lrj / gnj;
-        }
-        // ------------------------------------------------ BLS: the trial's fp32 iterate and its trajectory
-        // The reference evaluates each trial at its own fp32 iterate α_j = fl(fl(c_j·α) − fl(lr_j·ĝ))
-        // (optimizer_BLS.py:139-140).  [T; V] = L·α·J holds at the start of every trial (an accepted trial
-        // brings its exact trajectory along), so L·α_j·J = c_j·[T; V] − s_j·(L·G·J) + L·e_j·J with the
-        // iterate's rounding residual e_j = α_j − (c_j·α − s_j·G) (alpha_step, error-free): e_j goes
-        // through z = V_Rᵀ·e_j and F·z (rank 16) before the evaluation, so the trial is evaluated at α_j's
-        // own trajectory to fp32 resolution — not one rounding residual behind it.
-        // The residual enters the direction like the GD flows' (scaled by −1/s_j, stage 2's z): the trial's
-        // direction F·(y'' + z_j) with z_j = −V_Rᵀ·e_j/s_j, so c_j·[T; V] − s_j·(direction)·J is the
-        // trial's trajectory.  G comes from Gb, which every stage 2 rewrites with the same values for a
-        // trajectory in its line search (its gradient inputs in X are unchanged, and the stage-1 velocity
-        // half runs whenever a live trajectory's inputs have one, the dense flag): no per-lane latches.
-        if constexpr (BLS) {
-            if ((fl >> 30) & 1u) {  // block-uniform: some trajectory has a line-search trial this round
-                // (a trial that continues a line search had its iterate and residual formed at the end of the
-                // last round, before its barrier: the first barrier below runs only when some trajectory
-                // forms its trial here — a new direction's first trial (flag bit 27) or a helper)
-                if ((phase == LP_STEP && !pre_eb) || helper) {  // wave-uniform
-                    const float ne = -1.f / fmaxf(stepj, kMinRefStep);
-#pragma unroll
-                    for (int j = 0; j < WPL; ++j) {
-                        float G[D], eo[D];
-                        grad_alpha(j, G, helper ? ts : t);
-#pragma unroll
-                        for (int k = 0; k < D; ++k) {
-                            const float gh = G[k] / gnj;  // n_alpha_grad (optimizer_BLS.py:165)
-                            float er;
-                            aj[j][k] = alpha_step(al[j][k], cj, lrj, gh, stepj, G[k], er);
-                            eo[k] = er * ne;
-                        }
-                        if (wl[j]) {
-#pragma unroll
-                            for (int k = 0; k < D; ++k) Eb[(t * D + k) * lde + swz(nn[j], t * D + k)] = eo[k];
-                        }
-                    }
-                }
-                pre_eb = false;
-                if (((fl >> 27) & 1u) || hm) __syncthreads();
-                stage1z();
-                __syncthreads();
-                stage2f(std::true_type{}, std::false_type{});
-                __syncthreads();
-            }
+            stepj = div_rcp(lrj, gnj, rcp_refined(gnj));  // bls_gz's step, bit for bit
         }
         // ------------------------------------------------ end of an inner loop: α's exact trajectory
         if (rsy) {  // block-uniform
@@ -3080,7 +3293,15 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 if (f0.nl > h_loss - P.bls_a * h_lr0 * h_an && h_trial + 1 < P.max_bls) {
                     const Fin f1 = finalize(h_lsg, t);
                     if (!(f1.nl > h_loss - P.bls_a * h_lr * h_an)) {
-                        ss_write(ts, aj, q2, v2);  // t*'s α_j, T, V (adopted at the next round's start)
+                        // t*'s α_j (the trial stages' iterate of this slot's columns), T, V — adopted at the next
+                        // round's start; α_j also into t*'s α rows for the next trial stages
+                        float ajh[WPL][D];
+#pragma unroll
+                        for (int k = 0; k < D; ++k) {
+                            ajh[0][k] = Ajb[(t * D + k) * lde + swz(nn[0], t * D + k)];
+                            if (wl[0]) Ab[(ts * D + k) * lde + swz(nn[0], ts * D + k)] = ajh[0][k];
+                        }
+                        ss_write(ts, ajh, q2, v2);
                         if (!(h_loss - f1.nl < P.llr) && h_inner + 1 < P.max_inner) {
                             const bool bf = grad_inputs(w, q2, v2, f1.idx, h_lsg, h_ljl, ts);  // t*'s columns
                             if (lane == 0) {
@@ -3215,12 +3436,17 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 }
             }
             if (accept && BLS) {
-                // the trial's iterate α_j and its exact trajectory (optimizer_BLS.py:149)
+                // the trial's iterate α_j (formed by the trial stages, bls_gz) and its trajectory
+                // (optimizer_BLS.py:149); α_j into the α rows for the next trial stages
 #pragma unroll
                 for (int j = 0; j < WPL; ++j)
 #pragma unroll
                     for (int k = 0; k < D; ++k) {
-                        al[j][k] = aj[j][k];
+                        const int o = (t * D + k) * lde + swz(wl[j] ? nn[j] : 0, t * D + k);
+                        if (wl[j]) {
+                            al[j][k] = Ajb[o];
+                            Ab[o] = al[j][k];
+                        }
                         q[j][k] = q2[j][k];
                         v[j][k] = v2[j][k];
                     }
@@ -3265,28 +3491,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     }
                     needs_dir = true;
                 }
-                if constexpr (BLS) {
-                    // a rejected trial continues the line search: the next trial's iterate and residual now,
-                    // before the round's last barrier (optimizer_BLS.py:139-140 at lr·β₋; no barrier for them
-                    // at the next round's start)
-                    if (phase == LP_STEP && !needs_dir && !(kHelp && adopt)) {
-                        const float cn = unfused(1.f - unfused(P.lreg * lr)), sn = lr / gnorm;
-                        const float ne = -1.f / fmaxf(sn, kMinRefStep);
-                        float G[D], eo[D];
-                        grad_alpha(0, G, t);
-#pragma unroll
-                        for (int k = 0; k < D; ++k) {
-                            float er;
-                            aj[0][k] = alpha_step(al[0][k], cn, lr, G[k] / gnorm, sn, G[k], er);
-                            eo[k] = er * ne;
-                        }
-                        if (wl[0]) {
-#pragma unroll
-                            for (int k = 0; k < D; ++k) Eb[(t * D + k) * lde + swz(nn[0], t * D + k)] = eo[k];
-                        }
-                        pre_eb = true;
-                    }
-                }
+                if constexpr (BLS) ts_write();  // the next round's trial stages read lr and the phase
                 if constexpr (kHelp) {
                     // publish this trajectory's state for a helper: α, T, V when they changed (an accepted
                     // trial of its own, a new outer iteration's exact trajectory), the scalars every round
@@ -3308,7 +3513,6 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 if (lane == 0 && phase != LP_DONE)
                     atomicOr(&fw[par ^ 1], (1u << wave) | (needs_dir ? 1u << 28 : 0u) |
                                                (phase == LP_RESYNC ? 1u << 29 : 0u) | (phase == LP_STEP ? 1u << 30 : 0u) |
-                                               (BLS && phase == LP_STEP && !pre_eb ? 1u << 27 : 0u) |
                                                // BLS: every trajectory in a line search keeps the velocity
                                                // half on while its inputs have one (its Ypart / Gb columns
                                                // are recomputed by other trajectories' direction rounds)
@@ -3481,11 +3685,11 @@ struct type_tag {
 };
 
 // LDS of k_lean: the optimiser head + obstacles, no staged F fragments, the lean regions.
-inline size_t lean_lds(const KParams& p, bool help = false) {
+inline size_t lean_lds(const KParams& p, bool help = false, bool bls = false) {
     KParams q = p;
     q.regops = 1;
     return (size_t)lean_extra(plan_lds(q, false, true, true).total, p.MP, p.NK, p.RP, p.nsplit, lean_vlds(p.NK, p.D, p.BT),
-                              p.D, help ? p.BT : 0).total * 4;
+                              p.D, help ? p.BT : 0, bls).total * 4;
 }
 
 // The lean kernel's control flow for a launch (-1: the general kernel serves it): the GD single
@@ -3498,8 +3702,8 @@ inline int lean_flow(const KParams& p) {
 }
 // help: the launch's instantiation carries the BLS line-search helpers' exchange regions (lean_help), so
 // the check sees the LDS the launch will request (per-problem obstacle tables grow the base with TB·O)
-inline bool lean_fits(const KParams& p, bool help = false) {
-    return (p.RP / 16) * p.nsplit <= p.BT / 64 && p.NK / 16 <= 4 * p.nsplit && lean_lds(p, help) <= 160 * 1024;
+inline bool lean_fits(const KParams& p, bool help = false, bool bls = false) {
+    return (p.RP / 16) * p.nsplit <= p.BT / 64 && p.NK / 16 <= 4 * p.nsplit && lean_lds(p, help, bls) <= 160 * 1024;
 }
 
 // k_optimize<Shape> with the MAXT / operator-placement / optimiser variants (one shape per
@@ -3547,7 +3751,8 @@ hipError_t launch_lean_one(const KParams& p, int grid, hipStream_t s, LaunchDesc
         desc->rank_z = desc->rank_dir = 16;  // k_lean's per-stage ranks at RP = 32
         desc->rank_g = 24;
     }
-    return run_optimizer(desc, k_lean<Sh, TT, WPL, FULL, FLOW>, grid, p.BT, lean_lds(p, lean_help<Sh, TT, WPL, FULL, FLOW>()), s, p);
+    return run_optimizer(desc, k_lean<Sh, TT, WPL, FULL, FLOW>, grid, p.BT,
+                         lean_lds(p, lean_help<Sh, TT, WPL, FULL, FLOW>(), FLOW == LF_BLS), s, p);
 }
 
 template <class Sh, int TT, int WPL, bool FULL>
@@ -3572,14 +3777,15 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s, LaunchDesc* de
                 KParams q = p;
                 q.BT = p.BT / 2;
                 q.NW = p.NW / 2;
-                if (p.lean_wpl == 2 && flow == LF_GD1 && lean_fits(q))
+                if (p.lean_wpl == 2 && flow == LF_GD1 && lean_fits(q))  // (GD only)
                     return launch_lean_one<Sh, 256, 2, false, LF_GD1>(q, grid, s, desc);
             }
         }
         if constexpr (!Sh::kVariants && TT <= 512) {  // the lean kernel (F operators register-resident:
             // one stage-1 unit per wave; workgroups are padded to TT threads by choose_shape)
             const bool help = flow == LF_BLS && lean_help<Sh, TT, 1, true, LF_BLS>();
-            if (flow >= 0 && p.BT == TT && lean_fits(p, help)) return launch_lean_flow<Sh, TT, 1, true>(p, flow, grid, s, desc);
+            if (flow >= 0 && p.BT == TT && lean_fits(p, help, flow == LF_BLS))
+                return launch_lean_flow<Sh, TT, 1, true>(p, flow, grid, s, desc);
         }
         if constexpr (!Sh::kVariants && TT == 1024) {
             if constexpr (Sh::kNW == 256 && Sh::D * 3 <= kCols) {  // ≥ 3 trajectories fit the MFMA columns
@@ -3587,7 +3793,7 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s, LaunchDesc* de
                 KParams q = p;
                 q.BT = p.BT / 2;
                 q.NW = p.NW / 2;
-                if (flow >= 0 && lean_fits(q)) return launch_lean_flow<Sh, 512, 2, false>(q, flow, grid, s, desc);
+                if (flow >= 0 && lean_fits(q, false, flow == LF_BLS)) return launch_lean_flow<Sh, 512, 2, false>(q, flow, grid, s, desc);
             }
         }
         return launch_general_shape<Sh>(p, s, desc);
