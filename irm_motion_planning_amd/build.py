@@ -35,6 +35,7 @@ CFLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-fPIC", "-Wall", "-Wno
           "-ffp-contract=off", "-fno-slp-vectorize",
           "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
 FIX_SHAPES = [(3, 50), (3, 64), (3, 128), (3, 256), (7, 128), (7, 256)]  # IRM_FIX_SHAPES in irm_kernels_impl.hpp
+DENSE_SHAPES = [(7, 256)]  # the dense operator's k_lean (irm_kernels.hip launch_optimize)
 MAX_D = 8
 
 VARIANTS = {
@@ -100,6 +101,8 @@ def _units():
            + (ILP_SCHED if (d, n) in LEAN_ILP_SHAPES else [])) for d, n in FIX_SHAPES]
     u += [(f"opt_gen{d}_{n}", "irm_opt_inst.hip", [f"-DIRM_INST_GEN_D={d}", f"-DIRM_INST_GEN_N={n}"] + ILP_SCHED)
           for d, n in FIX_SHAPES]
+    u += [(f"opt_dense{d}_{n}", "irm_opt_inst.hip", [f"-DIRM_INST_DENSE_D={d}", f"-DIRM_INST_DENSE_N={n}"])
+          for d, n in DENSE_SHAPES]
     return u
 
 

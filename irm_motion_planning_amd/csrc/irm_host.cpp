@@ -720,6 +720,14 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
         kp.thr_hi = (float)((double)p->joint_safety_limit * (double)p->max_joint_position);
         kp.thr_lo = (float)((double)p->joint_safety_limit * (double)p->min_joint_position);
         kp.thr_v = (float)((double)p->joint_safety_limit * (double)p->max_joint_velocity);
+        // --constraint-violating-dependant-loss false (trajectory.py:221-222, 251: the penalties apply to
+        // every element): thresholds that every finite joint position / velocity passes, so the kernels
+        // form the masks without the flag (one scalar op fewer per mask element and round)
+        if (!p->constraint_violating_dependant_loss) {
+            kp.thr_hi = -INFINITY;
+            kp.thr_lo = INFINITY;
+            kp.thr_v = -1.f;
+        }
         kp.invN = 1.f / (float)N;
         kp.inv_std_pos = 1.f / kp.std_pos;
         kp.inv_vmax = 1.f / kp.vmax;

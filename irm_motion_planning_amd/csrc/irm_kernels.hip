@@ -6,6 +6,7 @@
 namespace irm {
 
 IRM_FIX_SHAPES(IRM_EXTERN_FIX)
+IRM_EXTERN_DENSE(7, 256)
 IRM_EXTERN_DYN(1) IRM_EXTERN_DYN(2) IRM_EXTERN_DYN(3) IRM_EXTERN_DYN(4)
 IRM_EXTERN_DYN(5) IRM_EXTERN_DYN(6) IRM_EXTERN_DYN(7) IRM_EXTERN_DYN(8)
 
@@ -107,6 +108,13 @@ __global__ void k_init_alpha(KParams P, float* alpha_out) {
 }
 
 hipError_t launch_optimize(const KParams& p, hipStream_t s, LaunchDesc* desc) {
+    // the dense operator (--operator-rank -1) of BASELINE configs[4]'s shape (7-DoF, N = 256): k_lean's GD
+    // single loop over DenseShape (the other flows, workgroup sizes: the general kernel below)
+    if (p.v_ident && p.D == 7 && p.N == 256 && p.RP == p.NK && !p.whole_robot && p.lean_ok) {
+        bool served = false;
+        const hipError_t e = launch_dense_shape<DenseShape<7, 256>>(p, s, desc, &served);
+        if (served) return e;
+    }
     // shape-specialised kernels for the common configurations (auto rank R = 32)
     if (p.RP == 32 && p.nsplit == stage1_splits(p.NK) && !p.whole_robot) {
 #define IRM_TRY_FIX(D_, N_) \

@@ -252,7 +252,7 @@ constexpr int kHpW = 8;
 // bls: the BLS flow's regions — α rows (Ab, in e.eb's place), the trial iterate's rows (Aj), the z partials
 // (quad-major, lean_bls_nzp) and the per-slot trial scalars (TS) instead of the GD flows' e' / z regions
 __host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, int nsplit, bool vlds, int D = 0,
-                                            int help_threads = 0, bool bls = false) {
+                                            int help_threads = 0, bool bls = false, bool dense = false) {
     LeanX e{};
     int off = base;
     e.vt = e.vn = 0;
@@ -272,12 +272,12 @@ __host__ __device__ inline LeanX lean_extra(int base, int MP, int NK, int RP, in
         off += lean_bls_nzp(NK) * 256;
         e.ts = off;
         off += kMaxTraj * kTsW;
-    } else {
+    } else if (!dense) {
         e.zp = off;
         off += al4(lean_zsplit(nsplit, vlds) * 16 * lean_ldy(RP));
     }
-    e.gb = off;
-    off += al4(16 * lean_ld(NK));
+    e.gb = off;  // (dense: G is y'' itself — no G rows, no z partials)
+    if (!dense) off += al4(16 * lean_ld(NK));
     e.ep = off;
     off += kMaxTraj * 2 * kEpS;
     e.ep0 = off;  // one zero word (the endpoint MFMA's B for k = 2, 3)

@@ -250,8 +250,8 @@ __device__ __forceinline__ void lean_pen(const KParams& P, const float (&q)[D], 
         const bool m = (q[d] > P.thr_hi) || (q[d] < P.thr_lo);
         const float zv = v[d] * P.inv_vmax;
         const bool mv = fabsf(v[d]) > P.thr_v;
-        zm[d] = (P.cvdl && !m) ? 0.f : z;
-        zvm[d] = (P.cvdl && !mv) ? 0.f : zv;
+        zm[d] = m ? z : 0.f;  // (cvdl off: the host's thresholds make every mask true)
+        zvm[d] = mv ? zv : 0.f;
     }
 }
 
@@ -398,7 +398,7 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
         const float zv = v[d] * P.inv_vmax;
         const bool mv = fabsf(v[d]) > P.thr_v;
         if constexpr (LEAN) {
-            const float zm = (P.cvdl && !m) ? 0.f : z, zvm = (P.cvdl && !mv) ? 0.f : zv;
+            const float zm = m ? z : 0.f, zvm = mv ? zv : 0.f;  // (cvdl: folded into the thresholds)
             if constexpr (kLeanKeep<D>) {
                 w.zm[d] = zm;
                 w.zvm[d] = zvm;
@@ -406,8 +406,8 @@ __device__ __forceinline__ void eval_waypoint(const KParams& P, const float (&q)
             jp = fmaf(zm, zm, jp);
             jv = fmaf(zvm, zvm, jv);
         } else {
-            jp += (P.cvdl && !m) ? 0.f : 0.5f * (z * z);
-            jv += (P.cvdl && !mv) ? 0.f : 0.5f * (zv * zv);
+            jp += m ? 0.5f * (z * z) : 0.f;
+            jv += mv ? 0.5f * (zv * zv) : 0.f;
         }
         tx = fmaxf(tx, q[d]);
         tn = fminf(tn, q[d]);
@@ -485,9 +485,9 @@ __device__ __forceinline__ void grad_waypoint(const KParams& P, const WP<D>& w, 
         }
         float jpg = 0.f, jvg = 0.f;
         const bool m = (q[d] > P.thr_hi) || (q[d] < P.thr_lo);
-        if (!P.cvdl || m) jpg = ((q[d] - P.mean_pos) * P.inv_std2) * P.invN;
+        if (m) jpg = ((q[d] - P.mean_pos) * P.inv_std2) * P.invN;
         const bool mv = fabsf(v[d]) > P.thr_v;
-        if (!P.cvdl || mv) jvg = (v[d] * P.inv_vmax2) * P.invN;
+        if (mv) jvg = (v[d] * P.inv_vmax2) * P.invN;
         a[d] = fmaf(ljl, jpg, fmaf(lsg, sgp, fmaf(wx, w.jx[d], wy * w.jy[d])));
         b[d] = fmaf(lsg, sgv, ljl * jvg);
     }
@@ -922,6 +922,13 @@ __device__ __forceinline__ float div_rcp(float a, float b, float r) {
     return fmaf(fmaf(-q, b, a), r, q);
 }
 
+// One f32x4 of an operator fragment array through a buffer descriptor: the per-lane part of the address in
+// one VGPR (voff, shared by every load of a stream), the wave-uniform part (tile, k-quad) in soff — a
+// streamed operator holds no 64-bit address per load (the dense stages' unrolled k-loops spilled them)
+__device__ __forceinline__ f32x4 ld_frag(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
 // Smallest step a rounding residual is folded with (e' = −e/step): |e'| ≤ 1e-3·2^80 ≈ 1e21 stays
 // finite where a tiny BLS step (lr/‖G‖ after many rejected trials, or --gd-lr 0) would give ±inf.
 constexpr float kMinRefStep = 8.271806e-25f;  // 2^-80
@@ -979,15 +986,29 @@ struct FixShape {
     static constexpr int D = D_, N = N_, NK = (N_ + 15) / 16 * 16, MP = 2 * NK, RP = RP_;
     static constexpr int NW = (N_ + 63) / 64 * 64, WPT = NW / 64, NSPLIT = stage1_splits(NK);
     static constexpr bool kVariants = false;  // end-effector cost only (the reference's)
+    static constexpr bool kDense = false;
     static constexpr int kNW = NW;             // lanes per trajectory (0: only known at run time)
     // stage-1 k-quads per split-K unit when the split is even (else 0: checked per quad)
     static constexpr int KQU = (NK / 16) % NSPLIT == 0 ? (NK / 16) / NSPLIT : 0;
     __device__ explicit FixShape(const KParams&) {}
 };
+// The dense operator (--operator-rank -1: R = N, F = L = [K; dK], V_R = I, so G = y'' and z = e') of a
+// fixed shape, for k_lean's GD single loop: one split, every operator fragment streamed from L2.
+template <int D_, int N_>
+struct DenseShape {
+    static constexpr int D = D_, N = N_, NK = (N_ + 15) / 16 * 16, MP = 2 * NK, RP = NK;
+    static constexpr int NW = (N_ + 63) / 64 * 64, WPT = NW / 64, NSPLIT = 1;
+    static constexpr bool kVariants = false;
+    static constexpr bool kDense = true;
+    static constexpr int kNW = NW;
+    static constexpr int KQU = 0;
+    __device__ explicit DenseShape(const KParams&) {}
+};
 template <int D_>
 struct DynShape {
     static constexpr int D = D_;
     static constexpr bool kVariants = true;  // cost variants chosen at run time (whole_robot)
+    static constexpr bool kDense = false;
     static constexpr int kNW = 0;
     static constexpr int KQU = 0;
     int N, NK, MP, RP, NW, WPT, NSPLIT;
@@ -2016,7 +2037,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     static_assert(NWL % 64 == 0, "whole waves per trajectory");
     static_assert(WPL == 1 || (WPL == 2 && S::kNW > 0 && S::kNW == S::NK),
                   "two waypoints per lane: every lane's waypoints exist (N a multiple of 64)");
-    static_assert(S::RP == 32, "k_lean runs at operator rank 32 (stage 2's kR24 slot skip)");
+    // the dense operator (DenseShape: R = N, F = L, V_R = I) runs the GD single loop with its own stages
+    constexpr bool DENSE = S::kDense;
+    static_assert(S::RP == 32 || (DENSE && GD1 && WPL == 1 && FULL),
+                  "k_lean runs at operator rank 32 (stage 2's kR24 slot skip), or the dense operator's GD loop");
     extern __shared__ __attribute__((aligned(16))) float smem[];
     const S sh(P);
     const Head H = plan_head(sh.MP, sh.RP, sh.NSPLIT, true, true);
@@ -2060,7 +2084,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     float* obsL = smem + H.obs;
     const int nsplit = sh.NSPLIT, zsplit = lean_zsplit(sh.NSPLIT, VL);
     constexpr bool kHelp = lean_help<S, MAXT, WPL, FULL, FLOW>();
-    const LeanX LX = lean_extra(plan_lds(P, false, true, true).total, MP, NK, RP, nsplit, VL, D, kHelp ? MAXT : 0, BLS);
+    const LeanX LX = lean_extra(plan_lds(P, false, true, true).total, MP, NK, RP, nsplit, VL, D, kHelp ? MAXT : 0, BLS, DENSE);
     float* Eb = smem + LX.eb;  // e' rows [column][waypoint]
     float* Zp = smem + LX.zp;  // stage-1 partials of V_Rᵀ·e'
     float* Gb = smem + LX.gb;  // (V_R·y'')[waypoint] rows [column][waypoint]
@@ -2109,7 +2133,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 if (tile < MT2 && i < KQ2) a2[j * 2 + i] = g2[((size_t)tile * KQ2 + i) * 64 + lane];
             }
     };
-    load_ops();
+    if constexpr (!DENSE) load_ops();  // (DENSE: every operator fragment streamed from L2 in its stage)
     // The endpoint velocity rows b'[0], b'[N−1] (stage 1's operator Fᵀ has zero columns there, so that a
     // sparse round can skip the velocity half) enter y'' through one more MFMA per stage-1 row tile, on
     // the split-0 units: k = 0 ↔ b'[0], k = 1 ↔ b'[N−1], k = 2, 3 zero.  A = the operator's endpoint
@@ -2887,6 +2911,123 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         for (int j = 0; j < S2T; ++j)
             if (wave + j * nwaves < MT2) *reinterpret_cast<f32x4*>(dP + cl * ldx + (wave + j * nwaves) * 16 + r4x) = acc[j];
     };
+    // ---- the dense operator (DENSE: DenseShape, F = L = [K; dK], V_R = I — G is y'' and z is e').
+    // Stage 1, y'' = Fᵀ·[a'; b']: the N/16 row tiles of y'' over the waves, each over the whole k range
+    // (the position half; the velocity half in dense rounds) plus the endpoint velocity rows' MFMA (as the
+    // rank-32 kernel's split-0 units).  Stage 2, dP = F·(y'' + e'): the MP/16 row tiles of [T; V] over the
+    // waves, the B operand one quad of y'' + e' per k-quad from LDS.  Every operator fragment (Fᵀ, F:
+    // 512 KB each at N = 256) is streamed from L2 kDPF k-quads ahead of its MFMAs; a sched_barrier per
+    // k-quad keeps the compiler from hoisting the whole stream (its registers) up front.
+    constexpr int kDW = MAXT / 64;
+    constexpr int kD1 = DENSE ? (S::RP / 16 + kDW - 1) / kDW : 1;  // stage-1 row tiles per wave
+    constexpr int kD2 = DENSE ? (S::MP / 16 + kDW - 1) / kDW : 1;  // stage-2 row tiles per wave
+    constexpr int kDQ = DENSE ? S::NK / 16 : 1;                    // k-quads per half
+#ifdef IRM_X_DENSE_PF1
+    constexpr int kDPF = 1;
+#else
+    constexpr int kDPF = 2;                                        // prefetch depth (k-quads)
+#endif
+    float aepd[kD1];  // F_bot rows 0 / N−1 of the wave's stage-1 row tiles (the endpoint MFMA's A)
+#pragma unroll
+    for (int j = 0; j < kD1; ++j) {
+        const int tl = wave + j * kDW;
+        aepd[j] = 0.f;
+        if (DENSE && tl < RP / 16 && (lane >> 4) < 2) aepd[j] = P.Fbot[(size_t)((lane >> 4) ? N - 1 : 0) * RP + tl * 16 + (lane & 15)];
+    }
+    auto dense_stage1 = [&](bool full) {
+        const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
+        constexpr int KQ1c = S::MP / 16;
+        const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(P.F1p), 0, (int)(frag_floats(S::RP, S::MP) * 4), 0x00020000);
+        const int vo = lane * 16;
+#ifdef IRM_X_DENSE_GLOBAL
+        auto g1ld = [&](int tl, int kq) { (void)r1; (void)vo; return reinterpret_cast<const f32x4*>(P.F1p)[(size_t)(tl * KQ1c + kq) * 64 + lane]; };
+#else
+        auto g1ld = [&](int tl, int kq) { return ld_frag(r1, vo, ((tl * KQ1c + kq) * 64) * 16); };
+#endif
+        const float* xl = X + cl * ldx + r4x;
+        const float bep = smem[epoff];
+        f32x4 acc[kD1];
+#pragma unroll
+        for (int j = 0; j < kD1; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(aepd[j], bep, z4, 0, 0, 0);
+        auto half = [&](int kb) {  // k-quads kb … kb + kDQ − 1 of Fᵀ's MP columns
+            f32x4 a[kDPF][kD1], b[kDPF];
+#pragma unroll
+            for (int p = 0; p < kDPF; ++p) {
+#pragma unroll
+                for (int j = 0; j < kD1; ++j) a[p][j] = g1ld(wave + j * kDW, kb + p);
+                b[p] = *reinterpret_cast<const f32x4*>(xl + (kb + p) * 16);
+            }
+#pragma unroll
+            for (int kq = 0; kq < kDQ; ++kq) {
+                const int sl = kq % kDPF;
+                f32x4 ac[kD1];
+#pragma unroll
+                for (int j = 0; j < kD1; ++j) ac[j] = a[sl][j];
+                const f32x4 bc = b[sl];
+                if (kq + kDPF < kDQ) {
+#pragma unroll
+                    for (int j = 0; j < kD1; ++j) a[sl][j] = g1ld(wave + j * kDW, kb + kq + kDPF);
+                    b[sl] = *reinterpret_cast<const f32x4*>(xl + (kb + kq + kDPF) * 16);
+                }
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+#pragma unroll
+                    for (int j = 0; j < kD1; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[j][m], bc[m], acc[j], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        };
+        half(0);
+        if (full) half(kDQ);
+#pragma unroll
+        for (int j = 0; j < kD1; ++j)
+            *reinterpret_cast<f32x4*>(Ypart + cl * ldy + (wave + j * kDW) * 16 + r4x) = acc[j];
+    };
+    auto dense_stage2 = [&]() {
+        constexpr int KQ2c = S::RP / 16;
+        const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(P.F2p), 0, (int)(frag_floats(S::MP, S::RP) * 4), 0x00020000);
+        const int vo = lane * 16;
+#ifdef IRM_X_DENSE_GLOBAL
+        auto g2ld = [&](int tl, int kq) { (void)r2; (void)vo; return reinterpret_cast<const f32x4*>(P.F2p)[(size_t)(tl * KQ2c + kq) * 64 + lane]; };
+#else
+        auto g2ld = [&](int tl, int kq) { return ld_frag(r2, vo, ((tl * KQ2c + kq) * 64) * 16); };
+#endif
+        const float* yl = Ypart + cl * ldy + r4x;
+        const float* el = Eb + cl * lde + r4x;
+        f32x4 acc[kD2], a[kDPF][kD2], by[kDPF], be[kDPF];
+#pragma unroll
+        for (int j = 0; j < kD2; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int p = 0; p < kDPF; ++p) {
+#pragma unroll
+            for (int j = 0; j < kD2; ++j) a[p][j] = g2ld(wave + j * kDW, p);
+            by[p] = *reinterpret_cast<const f32x4*>(yl + p * 16);
+            be[p] = *reinterpret_cast<const f32x4*>(el + p * 16);
+        }
+#pragma unroll
+        for (int kq = 0; kq < kDQ; ++kq) {
+            const int sl = kq % kDPF;
+            f32x4 ac[kD2];
+#pragma unroll
+            for (int j = 0; j < kD2; ++j) ac[j] = a[sl][j];
+            const f32x4 bt = by[sl] + be[sl];  // y'' + e' (z = V_Rᵀ·e' = e')
+            if (kq + kDPF < kDQ) {
+#pragma unroll
+                for (int j = 0; j < kD2; ++j) a[sl][j] = g2ld(wave + j * kDW, kq + kDPF);
+                by[sl] = *reinterpret_cast<const f32x4*>(yl + (kq + kDPF) * 16);
+                be[sl] = *reinterpret_cast<const f32x4*>(el + (kq + kDPF) * 16);
+            }
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int j = 0; j < kD2; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[j][m], bt[m], acc[j], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = 0; j < kD2; ++j)
+            *reinterpret_cast<f32x4*>(dP + cl * ldx + (wave + j * kDW) * 16 + r4x) = acc[j];
+    };
     // this lane's direction rows Δ = (F·y'')·J for waypoint j (the endpoint velocity rows are in y'')
     auto direction = [&](int j, float (&dt)[D], float (&dv)[D]) {
         float ut[D], uv[D];
@@ -2911,7 +3052,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     auto grad_alpha = [&](int j, float (&G)[D], int gt) {  // gt: the trajectory slot whose G is read
         const int r = wl[j] ? nn[j] : 0;  // (valid trajectories only)
 #pragma unroll
-        for (int k = 0; k < D; ++k) G[k] = Gb[(gt * D + k) * lde + swz(r, gt * D + k)];
+        for (int k = 0; k < D; ++k) {
+            if constexpr (DENSE) G[k] = Ypart[(gt * D + k) * ldy + swz(r, gt * D + k)];  // V_R = I: G = y''
+            else G[k] = Gb[(gt * D + k) * lde + swz(r, gt * D + k)];
+        }
     };
     auto snapshot = [&](irm_stats& st) {  // extended-vis frame after a non-breaking inner iteration
         if (rec && st.series_len < P.max_series) {
@@ -3120,12 +3264,17 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         if constexpr (!BLS) {
             if (dirr) {  // block-uniform
                 IRM_COUNT(13, dense);
-                stage1(dense, pre1, pre1w, pre1e);
-                stage1z();
+                if constexpr (DENSE) {
+                    dense_stage1(dense);
+                } else {
+                    stage1(dense, pre1, pre1w, pre1e);
+                    stage1z();
+                }
                 IRM_STAMP(1);
                 __syncthreads();
                 IRM_STAMP(2);
-                stage2f(std::true_type{}, std::true_type{});
+                if constexpr (DENSE) dense_stage2();
+                else stage2f(std::true_type{}, std::true_type{});
                 IRM_STAMP(3);
                 __syncthreads();
                 IRM_STAMP(4);
@@ -3685,11 +3834,11 @@ struct type_tag {
 };
 
 // LDS of k_lean: the optimiser head + obstacles, no staged F fragments, the lean regions.
-inline size_t lean_lds(const KParams& p, bool help = false, bool bls = false) {
+inline size_t lean_lds(const KParams& p, bool help = false, bool bls = false, bool dense = false) {
     KParams q = p;
     q.regops = 1;
     return (size_t)lean_extra(plan_lds(q, false, true, true).total, p.MP, p.NK, p.RP, p.nsplit, lean_vlds(p.NK, p.D, p.BT),
-                              p.D, help ? p.BT : 0, bls).total * 4;
+                              p.D, help ? p.BT : 0, bls, dense).total * 4;
 }
 
 // The lean kernel's control flow for a launch (-1: the general kernel serves it): the GD single
@@ -3713,7 +3862,8 @@ hipError_t launch_general_shape(const KParams& p, hipStream_t s, LaunchDesc* des
 
 template <class Sh>
 inline int shape_name(char* buf, size_t n) {
-    if constexpr (Sh::kNW > 0) return snprintf(buf, n, "FixShape<%d,%d,%d>", Sh::D, Sh::N, Sh::RP);
+    if constexpr (Sh::kDense) return snprintf(buf, n, "DenseShape<%d,%d>", Sh::D, Sh::N);
+    else if constexpr (Sh::kNW > 0) return snprintf(buf, n, "FixShape<%d,%d,%d>", Sh::D, Sh::N, Sh::RP);
     else return snprintf(buf, n, "DynShape<%d>", Sh::D);
 }
 inline const char* flow_name(int flow) { return flow == LF_GD1 ? "GD1" : flow == LF_GD2 ? "GD2" : "BLS"; }
@@ -3750,9 +3900,13 @@ hipError_t launch_lean_one(const KParams& p, int grid, hipStream_t s, LaunchDesc
         desc->wpl = WPL;
         desc->rank_z = desc->rank_dir = 16;  // k_lean's per-stage ranks at RP = 32
         desc->rank_g = 24;
+        if constexpr (Sh::kDense) {  // V_R = I: G is y'' and z is e' (no MFMAs), the direction at rank N
+            desc->rank_z = desc->rank_g = 0;
+            desc->rank_dir = Sh::RP;
+        }
     }
     return run_optimizer(desc, k_lean<Sh, TT, WPL, FULL, FLOW>, grid, p.BT,
-                         lean_lds(p, lean_help<Sh, TT, WPL, FULL, FLOW>(), FLOW == LF_BLS), s, p);
+                         lean_lds(p, lean_help<Sh, TT, WPL, FULL, FLOW>(), FLOW == LF_BLS, Sh::kDense), s, p);
 }
 
 template <class Sh, int TT, int WPL, bool FULL>
@@ -3804,6 +3958,21 @@ hipError_t launch_optimize_shape(const KParams& p, hipStream_t s, LaunchDesc* de
 // own unit (irm_opt_inst.hip, IRM_INST_GEN_*) so that build.py can compile it with the
 // iterative-ILP machine scheduler, which measured 10 % faster on it (faithful C3) while the lean
 // kernels keep the default scheduler.
+// The dense operator's k_lean (DenseShape, GD single loop, one 512-thread workgroup of TB trajectories):
+// *served = false leaves the launch to the general kernel (another workgroup size, LDS).
+template <class Sh>
+hipError_t launch_dense_shape(const KParams& p, hipStream_t s, LaunchDesc* desc, bool* served) {
+    *served = false;
+    if (p.BT != 512 || p.TB * Sh::D > kCols || lean_flow(p) != LF_GD1) return hipSuccess;
+    KParams q = p;
+    q.nsplit = 1;  // one split: every wave's stage-1 row tiles over the whole k range
+    if (lean_lds(q, false, false, true) > 160 * 1024) return hipSuccess;
+    *served = true;
+    const int grid = (p.B + p.TB - 1) / p.TB;
+    if (grid <= 0) return hipSuccess;
+    return launch_lean_one<Sh, 512, 1, true, LF_GD1>(q, grid, s, desc);
+}
+
 template <class Sh>
 hipError_t launch_general_shape(const KParams& p, hipStream_t s, LaunchDesc* desc) {
     const bool stage = p.ops_in_lds != 0;
@@ -3864,6 +4033,8 @@ hipError_t launch_forward_dim(const KParams& p, int mode, hipStream_t s) {
 #define IRM_FIX_SHAPES(X) X(3, 50) X(3, 64) X(3, 128) X(3, 256) X(7, 128) X(7, 256)
 #define IRM_EXTERN_FIX(D_, N_) \
     extern template hipError_t launch_optimize_shape<FixShape<D_, N_, 32>>(const KParams&, hipStream_t, LaunchDesc*);
+#define IRM_EXTERN_DENSE(D_, N_) \
+    extern template hipError_t launch_dense_shape<DenseShape<D_, N_>>(const KParams&, hipStream_t, LaunchDesc*, bool*);
 #define IRM_EXTERN_DYN(D_)                                                                                      \
     extern template hipError_t launch_optimize_shape<DynShape<D_>>(const KParams&, hipStream_t, LaunchDesc*); \
     extern template hipError_t launch_forward_dim<D_>(const KParams&, int, hipStream_t);

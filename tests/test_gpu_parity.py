@@ -381,6 +381,16 @@ def _bench_vs_ref(cfg, B, n_check, iters=200, lmax=None, argmod=None, operator_r
     return c, alpha, traj, st
 
 
+def test_penalties_without_violation_masks_track_oracle():
+    """--constraint-violating-dependant-loss false (trajectory.py:221-222, 251: the joint-limit penalties
+    on every element, not only where the 0.98 limits are exceeded): the host folds the flag into the mask
+    thresholds (every finite value passes), the kernels form the masks without it.  100 bench-mode GD
+    steps at C3's shape inside the oracle band (the oracle applies the flag as the reference does)."""
+    def mod(a):
+        a.constraint_violating_dependant_loss = False
+    _bench_vs_ref("c3", 64, 4, iters=100, argmod=mod, want_kernel="k_lean")
+
+
 @pytest.mark.parametrize("cfg,B", [("c3", 256), ("c4", 32), ("c5", 16), ("c7", 32)])
 def test_bench_smooth_objective_tracks_oracle(cfg, B):
     """λmax = 0 (mean obstacle cost only): 200 steps inside the oracle band."""
@@ -448,16 +458,50 @@ def test_launch_plan_names_the_dispatched_kernel(cfg, faithful, B, want):
 
 
 def test_dense_operator_plan_skips_identity_g_tiles():
-    """--operator-rank -1 (F = L, V_R = I): the general kernel at R = N forms G = V_R·y'' as the y'' rows
-    themselves and z = V_Rᵀ·e' as e' (no MFMAs on the identity), and the plan says so (rank_g = rank_z
-    = 0), so bench's executed-flop count excludes them."""
+    """--operator-rank -1 (F = L, V_R = I): G = V_R·y'' is the y'' rows themselves and z = V_Rᵀ·e' is e'
+    (no MFMAs on the identity), and the plan says so (rank_g = rank_z = 0), so bench's executed-flop count
+    excludes them.  C5's shape (7-DoF, N = 256) runs the dense operator's k_lean (DenseShape, GD single
+    loop); the dual loop and other shapes the general kernel."""
     import bench
     from irm_motion_planning_amd.context import Context
     from irm_motion_planning_amd.params import params_from_args
     c = Context(params_from_args(bench.make_args("c5", False, 200), operator_rank=-1))
     pl = c.launch_plan(512, bench.CONFIGS["c5"][4])
+    assert pl["kernel"] == "k_lean<DenseShape<7,256>,512,1,FULL,GD1>" and pl["lean"], pl
+    assert (pl["rank_z"], pl["rank_dir"], pl["rank_g"]) == (0, 256, 0), pl
+    c = Context(params_from_args(bench.make_args("c5", True, 200), operator_rank=-1))
+    pl = c.launch_plan(512, bench.CONFIGS["c5"][4])
     assert pl["kernel"].startswith("k_optimize") and not pl["lean"], pl
     assert (pl["rank_z"], pl["rank_dir"], pl["rank_g"]) == (0, 256, 0), pl
+
+
+def test_dense_lean_kernel_tracks_general_kernel(monkeypatch):
+    """The dense operator's k_lean (stages over all waves, operator fragments streamed from L2) against
+    the general kernel at R = N on the same 32 C5 problems and α0, 100 bench-mode GD steps: the same
+    iteration (fp32 α with the reference's rounding, the rounding residual through z = e'); the two
+    differ only in the MFMA summation order of the contractions (split-K partials vs one chain per row
+    tile), so the trajectories agree to the fp32 noise of K@α, not bit for bit — within N256_ORACLE_FLOOR
+    (the N = 256 max-cost near-ties below; measured: max 4.8e-3, median 1.1e-4, loss 7e-5 relative)."""
+    import bench
+    from irm_motion_planning_amd.context import Context
+    from irm_motion_planning_amd.params import params_from_args
+    B, iters = 32, 100
+    args = bench.make_args("c5", False, iters)
+    s, g, obs = bench.make_problem("c5", 1, 0)
+    s, g = s[:B], g[:B]
+    cl = Context(params_from_args(args, operator_rank=-1))
+    assert cl.launch_plan(B, len(obs))["kernel"].startswith("k_lean<DenseShape<7,256>")
+    a0 = cl.init_alpha(s, g)
+    al, tl, stl = cl.optimize(s, g, obs, alpha0=a0)
+    monkeypatch.setenv("IRM_GENERAL_KERNEL", "1")
+    cg = Context(params_from_args(args, operator_rank=-1))
+    assert cg.launch_plan(B, len(obs))["kernel"].startswith("k_optimize")
+    ag, tg, stg = cg.optimize(s, g, obs, alpha0=a0)
+    err = np.abs(tl - tg).reshape(B, -1).max(axis=1)
+    rel = np.abs(stl["final_loss"] - stg["final_loss"]) / np.abs(stg["final_loss"])
+    print(f"dense lean vs general: |traj| max {err.max():.2e} median {np.median(err):.2e}, loss rel max {rel.max():.2e}")
+    assert np.all(stl["grad_evals"] == iters) and np.all(stg["grad_evals"] == iters)
+    assert err.max() <= N256_ORACLE_FLOOR and rel.max() <= 1e-4, (err.max(), rel.max())
 
 
 @pytest.mark.parametrize("sigma,rank", [(0.07, 0), (0.1, 32)])
@@ -511,7 +555,8 @@ def test_dense_operator_at_n256(cfg):
     cd = Context(params_from_args(args, operator_rank=-1))
     c32 = Context(params_from_args(args))
     pl = cd.launch_plan(B, len(obs))
-    assert cd.info()["operator_rank"] == 256 and pl["rank_dir"] == 256 and pl["kernel"].startswith("k_optimize"), pl
+    want = "k_lean<DenseShape<7,256>" if cfg == "c5" else "k_optimize"  # (C3 problems at N = 256: D = 3)
+    assert cd.info()["operator_rank"] == 256 and pl["rank_dir"] == 256 and pl["kernel"].startswith(want), pl
     assert c32.info()["operator_rank"] == 32
     a0 = cd.init_alpha(s, g)
     _, td, std = cd.optimize(s, g, obs, alpha0=a0)
