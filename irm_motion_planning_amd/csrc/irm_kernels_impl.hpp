@@ -2922,11 +2922,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     constexpr int kD1 = DENSE ? (S::RP / 16 + kDW - 1) / kDW : 1;  // stage-1 row tiles per wave
     constexpr int kD2 = DENSE ? (S::MP / 16 + kDW - 1) / kDW : 1;  // stage-2 row tiles per wave
     constexpr int kDQ = DENSE ? S::NK / 16 : 1;                    // k-quads per half
-#ifdef IRM_X_DENSE_PF1
-    constexpr int kDPF = 1;
-#else
-    constexpr int kDPF = 2;                                        // prefetch depth (k-quads)
-#endif
+    constexpr int kDPF = 2;  // prefetch depth (k-quads; 3 and 4 measured the same: the stages are MFMA-bound)
     float aepd[kD1];  // F_bot rows 0 / N−1 of the wave's stage-1 row tiles (the endpoint MFMA's A)
 #pragma unroll
     for (int j = 0; j < kD1; ++j) {
@@ -2940,11 +2936,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<float*>(P.F1p), 0, (int)(frag_floats(S::RP, S::MP) * 4), 0x00020000);
         const int vo = lane * 16;
-#ifdef IRM_X_DENSE_GLOBAL
-        auto g1ld = [&](int tl, int kq) { (void)r1; (void)vo; return reinterpret_cast<const f32x4*>(P.F1p)[(size_t)(tl * KQ1c + kq) * 64 + lane]; };
-#else
         auto g1ld = [&](int tl, int kq) { return ld_frag(r1, vo, ((tl * KQ1c + kq) * 64) * 16); };
-#endif
         const float* xl = X + cl * ldx + r4x;
         const float bep = smem[epoff];
         f32x4 acc[kD1];
@@ -2988,11 +2980,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<float*>(P.F2p), 0, (int)(frag_floats(S::MP, S::RP) * 4), 0x00020000);
         const int vo = lane * 16;
-#ifdef IRM_X_DENSE_GLOBAL
-        auto g2ld = [&](int tl, int kq) { (void)r2; (void)vo; return reinterpret_cast<const f32x4*>(P.F2p)[(size_t)(tl * KQ2c + kq) * 64 + lane]; };
-#else
         auto g2ld = [&](int tl, int kq) { return ld_frag(r2, vo, ((tl * KQ2c + kq) * 64) * 16); };
-#endif
         const float* yl = Ypart + cl * ldy + r4x;
         const float* el = Eb + cl * lde + r4x;
         f32x4 acc[kD2], a[kDPF][kD2], by[kDPF], be[kDPF];

@@ -30,6 +30,8 @@ LEAN_PHASES = ["round top: flags + latch reads", "stage-1 MFMA", "stage-1 barrie
 
 
 def run(cfg, tb=0, rank=0, faithful=False):
+    if faithful:  # k_lean's BLS flow reports each problem's kernel rounds (trace_b bit 29, series_len)
+        os.environ["IRM_TRACE_PROBLEM"] = str(1 << 29)
     args = bench.make_args(cfg, faithful, 200)
     start, goal, obstacles = bench.make_problem(cfg, 1, 0)
     ctx = Context(params_from_args(args, traj_per_block=tb, operator_rank=rank))
@@ -48,15 +50,27 @@ def run(cfg, tb=0, rank=0, faithful=False):
     tot = prof.sum(1) - prof[:, 13]
     print(f"== {cfg} tb={info['traj_per_block']} R={info['operator_rank']} blocks={n} host {1000*dt:.2f} ms "
           f"rounds~{rounds:.0f} total cycles/block mean {tot.mean():.0f} -> {tot.mean()/rounds:.0f} per round")
-    for i, name in enumerate(LEAN_PHASES if os.environ.get("IRM_PROFILE_LEAN") else PHASES):
+    names = LEAN_PHASES if os.environ.get("IRM_PROFILE_LEAN") else PHASES
+    for i, name in enumerate(names):
         c = prof[:, i].mean()
         if i == 13:
             print(f"   {name:22s} {c:9.1f} of {rounds:.0f} rounds")
         elif c > 0:
             print(f"   {name:22s} {c/rounds:9.0f} cyc/round  ({100*c/tot.mean():5.1f} %)")
+    if faithful:  # the block that bounds the launch: its own rounds (its slowest problem's kernel rounds)
+        k = int(np.argmax(tot))
+        tbk = info["traj_per_block"]
+        kr = (st["series_len"][k * tbk:(k + 1) * tbk] & 0xFFFF).max() if args.optimizer_name == "bls" else 0
+        kr = float(kr) if kr > 0 else rounds
+        print(f"   slowest block {k}: {tot[k]:.0f} cycles, {kr:.0f} kernel rounds -> {tot[k] / kr:.0f} per round")
+        for i, name in enumerate(names):
+            c = prof[k, i]
+            if i != 13 and c > 0:
+                print(f"     {name:22s} {c/kr:9.0f} cyc/round  ({100*c/tot[k]:5.1f} %)")
 
 
 if __name__ == "__main__":
     for cfg in sys.argv[1:] or ["c3", "c2", "c5"]:  # "c5@-1": config at --operator-rank -1 (dense)
-        name, _, rank = cfg.partition("@")
-        run(name, rank=int(rank) if rank else 0)
+        faithful = cfg.endswith("!f")  # "c3bls!f": the reference's control flow
+        name, _, rank = cfg.rstrip("!f").partition("@")
+        run(name, rank=int(rank) if rank else 0, faithful=faithful)
