@@ -2094,6 +2094,20 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     static_assert(D <= kEpS, "endpoint rows fit their slots");
     const float* VT = VL ? smem + LX.vt : P.VTp;
     const float* VN = VL ? smem + LX.vn : P.VNp;
+    // V_R fragment quad q (VT: V_Rᵀ for z, VN: V_R for G): from LDS when staged there, else from L2 through a
+    // buffer descriptor — the lane's offset in one VGPR, the wave-uniform quad offset in an SGPR, so a wave's
+    // batch of fragment loads holds no 64-bit address per load (at N = 256 those spilled)
+    const unsigned vbytes = (unsigned)(frag_floats(RP, NK) * 4);
+    const __amdgpu_buffer_rsrc_t rVT = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(P.VTp), 0, (int)vbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rVN = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(P.VNp), 0, (int)vbytes, 0x00020000);
+    auto vt_frag = [&](int q) -> f32x4 {
+        if constexpr (VL) return reinterpret_cast<const f32x4*>(VT)[(size_t)q * 64 + lane];
+        else return ld_frag(rVT, lane * 16, q * 1024);
+    };
+    auto vn_frag = [&](int q) -> f32x4 {
+        if constexpr (VL) return reinterpret_cast<const f32x4*>(VN)[(size_t)q * 64 + lane];
+        else return ld_frag(rVN, lane * 16, q * 1024);
+    };
 
     const int KQ1 = MP / 16, KQa = NK / 16, MT1 = RP / 16, KQ2 = RP / 16, MT2 = MP / 16, MTG = NK / 16;
     const int ldx = MP + 8, ldy = lean_ldy(RP), lde = lean_ld(NK);  // column strides, all ≡ 8 mod 64
@@ -2503,11 +2517,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             constexpr int KQZ = kKQa / kZS;
             const int sp = nwaves - 1 - wave;
             if (sp >= kZS) return;
-            const f32x4* ap = reinterpret_cast<const f32x4*>(VT) + lane + (size_t)(sp * KQZ) * 64;
             f32x4 a[KQZ], bb[KQZ];
 #pragma unroll
             for (int i = 0; i < KQZ; ++i) {
-                a[i] = ap[(size_t)i * 64];
+                a[i] = vt_frag(sp * KQZ + i);
                 bb[i] = *reinterpret_cast<const f32x4*>(el + (sp * KQZ + i) * 16);
             }
             if constexpr (kLatS) __builtin_amdgcn_sched_barrier(0);  // all loads in flight before the first MFMA
@@ -2524,10 +2537,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         }
         for (int sp = nwaves - 1 - wave; sp < zsplit; sp += nwaves) {
             const int k0 = (KQa * sp) / zsplit, k1 = (KQa * (sp + 1)) / zsplit;
-            const f32x4* ap = reinterpret_cast<const f32x4*>(VT) + lane;
             f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
             for (int kq = k0; kq < k1; ++kq) {
-                const f32x4 a = ap[(size_t)kq * 64];
+                const f32x4 a = vt_frag(kq);
                 const f32x4 bb = *reinterpret_cast<const f32x4*>(el + kq * 16);
                 acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], bb[0], acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], bb[1], acc1, 0, 0, 0);
@@ -2563,11 +2575,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
             for (int g = 0; g < kGT; ++g) {
                 const int u = nwaves - 1 - wave + g * nwaves;
-                const f32x4* ap = reinterpret_cast<const f32x4*>(VN) + (size_t)u * KQ2 * 64 + lane;
                 ga[g][0] = ga[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
                 if (u < kMTG) {
-                    ga[g][0] = ap[0];
-                    ga[g][1] = ap[64];
+                    ga[g][0] = vn_frag(u * KQ2);
+                    ga[g][1] = vn_frag(u * KQ2 + 1);
                 }
             }
         }
@@ -2676,12 +2687,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         }
         // G tiles (waypoint rows of V_R·y''), from the top wave down
         for (int u = nwaves - 1 - wave; WG && u < MTG; u += nwaves) {
-            const f32x4* ap = reinterpret_cast<const f32x4*>(VN) + (size_t)u * KQ2 * 64 + lane;
             f32x4 ag = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
                 if (i < KQ2) {
-                    const f32x4 a = ap[(size_t)i * 64];
+                    const f32x4 a = vn_frag(u * KQ2 + i);
 #pragma unroll
                     for (int m = 0; m < (i == 1 ? 2 : 4); ++m)  // kR24
                         ag = __builtin_amdgcn_mfma_f32_16x16x4f32(a[m], by[i][m], ag, 0, 0, 0);
@@ -2703,7 +2713,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // lane's column reads.
     constexpr int kNZP = lean_bls_nzp(S::kNW > 0 ? S::NK : 256);
     const int nzp = min(nwaves, MTG);  // z partials (one per G-tile wave)
-    constexpr bool kBFix = FULL && S::kNW > 0;
+    // (fixed shapes up to N = 128: at N = 256 the batch's per-tile operands — four tiles per wave at 256
+    // threads — pushed the BLS variants into scratch; those take the per-tile loop, same sums in the same order)
+    constexpr bool kBFix = FULL && S::kNW > 0 && S::NK <= 128;
     constexpr int kNZc = kBFix ? (MAXT / 64 < S::NK / 16 ? MAXT / 64 : S::NK / 16) : 1;
     static_assert(!BLS || !kBFix || kNZc <= kNZP, "z partials fit their region");
     float* Ab = smem + LX.eb;    // BLS: α rows [column][waypoint] (Eb's place)
@@ -2731,7 +2743,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 Ap[g] = Vp[g] = Gt[g] = f32x4{0.f, 0.f, 0.f, 0.f};
                 if (u < S::NK / 16) {
                     Ap[g] = *reinterpret_cast<const f32x4*>(Ab + ycl * lde + u * 16 + r4y);
-                    Vp[g] = reinterpret_cast<const f32x4*>(VT)[(size_t)u * 64 + lane];
+                    Vp[g] = vt_frag(u);
                     if constexpr (!fresh) Gt[g] = *reinterpret_cast<const f32x4*>(Gb + ycl * lde + u * 16 + r4y);
                 }
             }
@@ -2749,11 +2761,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 }
 #pragma unroll
                 for (int g = 0; g < kT; ++g) {
-                    const f32x4* ap = reinterpret_cast<const f32x4*>(VN) + (size_t)(pz + g * (MAXT / 64)) * KQ2 * 64 + lane;
+                    const int u = pz + g * (MAXT / 64);
                     gv[g][0] = gv[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-                    if (pz + g * (MAXT / 64) < S::NK / 16) {
-                        gv[g][0] = ap[0];
-                        gv[g][1] = ap[64];
+                    if (u < S::NK / 16) {
+                        gv[g][0] = vn_frag(u * KQ2);
+                        gv[g][1] = vn_frag(u * KQ2 + 1);
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -2802,8 +2814,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             gn = __builtin_amdgcn_sqrtf(g2);  // v_sqrt_f32 (≤ 1 ulp): every user reads this value (TS)
             if (pz == 0 && lane < kCols && ycl == cl && cl % D == 0) TS[(cl / D) * kTsW + 1] = gn;  // for the trajectories and the later rounds
             if constexpr (!kBFix) {
-                const f32x4* ap = reinterpret_cast<const f32x4*>(VN) + (size_t)pz * KQ2 * 64 + lane;
-                const f32x4 g0 = ap[0], g1 = ap[64];
+                const f32x4 g0 = vn_frag(pz * KQ2), g1 = vn_frag(pz * KQ2 + 1);
                 Gt[0] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
                 for (int m = 0; m < 4; ++m) Gt[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(g0[m], y0[m], Gt[0], 0, 0, 0);
@@ -2852,8 +2863,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 if (fresh && u == pz) {
                     G = Gt[0];
                 } else if (fresh) {  // further tiles of the wave (general launches)
-                    const f32x4* ap = reinterpret_cast<const f32x4*>(VN) + (size_t)u * KQ2 * 64 + lane;
-                    const f32x4 g0 = ap[0], g1 = ap[64];
+                    const f32x4 g0 = vn_frag(u * KQ2), g1 = vn_frag(u * KQ2 + 1);
                     f32x4 y0 = *reinterpret_cast<const f32x4*>(Ypart + ycl * ldy + r4y);
                     f32x4 y1 = *reinterpret_cast<const f32x4*>(Ypart + ycl * ldy + 16 + r4y);
                     for (int sp = 1; sp < nsplit; ++sp) {
@@ -2869,7 +2879,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     G = *reinterpret_cast<const f32x4*>(Gb + ycl * lde + u * 16 + r4y);
                 }
                 tile(u, G, fresh, *reinterpret_cast<const f32x4*>(Ab + ycl * lde + u * 16 + r4y),
-                     reinterpret_cast<const f32x4*>(VT)[(size_t)u * 64 + lane]);
+                     vt_frag(u));
             }
         }
         *reinterpret_cast<f32x4*>(Zq + pz * 256 + (r4 >> 2) * 64 + cl * 4) = acc0 + acc1;
