@@ -649,6 +649,29 @@ def test_per_problem_obstacles_and_edge_counts():
                 assert int(st["grad_evals"][b]) == so["grad_evals"]
 
 
+def test_bls_helper_kernel_with_per_problem_obstacle_tables():
+    """Per-problem obstacle tables grow the lean kernel's LDS by TB·O·2 floats, and the BLS helper regions
+    come on top (lean_fits counts both, as the launch does — round-4 advice).  C3-BLS (the helper
+    kernel, four trajectories per 512-thread workgroup) with 64 obstacles per problem, the maximum: the
+    launch must go through, and with every problem's table equal to one shared table the results must be
+    the shared table's bit for bit (the per-problem path changes only where the table is read)."""
+    import bench
+    from irm_motion_planning_amd.context import Context
+    from irm_motion_planning_amd.params import params_from_args
+    c = Context(params_from_args(bench.make_args("c3bls", True, 20)))
+    s, g, _ = bench.make_problem("c3bls", 1, 0)
+    B = 1024
+    rng = np.random.default_rng(17)
+    shared = rng.uniform(-3.5, 3.5, (64, 2)).astype(np.float32)
+    per = np.ascontiguousarray(np.broadcast_to(shared, (B, 64, 2)))
+    a_s, t_s, st_s = c.optimize(s[:B], g[:B], shared)
+    a_p, t_p, st_p = c.optimize(s[:B], g[:B], per, obstacle_stride=2 * 64)
+    np.testing.assert_array_equal(a_p, a_s)
+    np.testing.assert_array_equal(t_p, t_s)
+    for k in ("grad_evals", "bls_trials", "outer_iterations"):
+        np.testing.assert_array_equal(st_p[k], st_s[k])
+
+
 def test_device_pointer_entry_point():
     """irm_optimize_batch_dev on torch-allocated HBM (the bench path) == host entry point."""
     import torch
