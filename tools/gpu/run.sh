@@ -71,9 +71,10 @@ case "$cmd" in
   sq)
     cd /tmp && export TMPDIR=/tmp
     for v in ${1:-release}; do
+      d="$OUT/sq_${v}_$(tag_of "${2:-c3}")"
       IRM_LIB=$(lib_of $v) timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU \
-        --output-format csv -d "$OUT/sq_$v" -o run -- python3 "$ROOT/bench.py" --no-cpu-baseline --steps 3 --warmup 1 --config ${2:-c3} > "$OUT/sq_$v.log" 2>&1 || { echo "pmc $v failed"; tail -3 "$OUT/sq_$v.log"; exit 3; }
-      echo "== $v"; python3 "$ROOT/tools/summarize_sq.py" "$OUT/sq_$v" | sed 's/^/   /'
+        --output-format csv -d "$d/p1" -o run -- python3 "$ROOT/bench.py" --no-cpu-baseline --steps 3 --warmup 1 --config ${2:-c3} > "$d.log" 2>&1 || { echo "pmc $v failed"; tail -3 "$d.log"; exit 3; }
+      echo "== $v ${2:-c3}"; python3 "$ROOT/tools/summarize_pmc_round.py" "$d" | sed 's/^/   /'
     done ;;
   phase)
     IRM_LIB=$ROOT/irm_motion_planning_amd/libirm_hip_prof.so IRM_PROFILE_LEAN=1 timeout -k 10 240 python tools/phase_profile.py ${1:-c3 c3bls} > "$OUT/phase.log" 2>&1
