@@ -2511,16 +2511,43 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // up front (one wait), then the MFMAs — the same accumulation order as the loop below
     constexpr int kZS = lean_zsplit(S::NSPLIT, VL), kKQa = S::NK / 16;
     constexpr bool kZFix = FULL && S::kNW > 0 && kKQa % kZS == 0 && kZS <= MAXT / 64;
+    constexpr int kKQZ = kZFix ? kKQa / kZS : 1;
+    constexpr int kMTG = S::NK / 16, kGT = (kMTG + MAXT / 64 - 1) / (MAXT / 64);
+    constexpr bool kS2Fix = FULL && S::kNW > 0;
+    // V_R staged in LDS (C3's shape), GD flows: the z unit's V_Rᵀ fragments and the G tiles' V_R fragments
+    // are the same every round — held in VGPRs for the launch instead of re-read from LDS each round
+    // (C3 faithful 3.93 -> 3.75 ms, C3 even; bit-identical)
+#ifdef IRM_X_VREGL2
+    // (from L2 too; not the 7-DoF N = 256 dual loop / 256-thread variants, which spill with them)
+    constexpr bool kVReg = !BLS && !DENSE && kZFix && kS2Fix && (VL || !(D > 3 && S::NK > 128) || (GD1 && MAXT > 256));
+#else
+    constexpr bool kVReg = !BLS && !DENSE && VL && kZFix && kS2Fix;
+#endif
+    f32x4 vtR[kVReg ? kKQZ : 1], vnR[kVReg ? kGT : 1][2];
+    if constexpr (kVReg) {
+        const int sp = nwaves - 1 - wave;
+#pragma unroll
+        for (int i = 0; i < kKQZ; ++i) vtR[i] = sp < kZS ? vt_frag(sp * kKQZ + i) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int g = 0; g < kGT; ++g) {
+            const int u = nwaves - 1 - wave + g * nwaves;
+            vnR[g][0] = vnR[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (u < kMTG) {
+                vnR[g][0] = vn_frag(u * KQ2);
+                vnR[g][1] = vn_frag(u * KQ2 + 1);
+            }
+        }
+    }
     auto stage1z = [&]() {
         const float* el = Eb + cl * lde + r4x;
         if constexpr (kZFix) {
-            constexpr int KQZ = kKQa / kZS;
+            constexpr int KQZ = kKQZ;
             const int sp = nwaves - 1 - wave;
             if (sp >= kZS) return;
             f32x4 a[KQZ], bb[KQZ];
 #pragma unroll
             for (int i = 0; i < KQZ; ++i) {
-                a[i] = vt_frag(sp * KQZ + i);
+                a[i] = kVReg ? vtR[i] : vt_frag(sp * KQZ + i);
                 bb[i] = *reinterpret_cast<const f32x4*>(el + (sp * KQZ + i) * 16);
             }
             if constexpr (kLatS) __builtin_amdgcn_sched_barrier(0);  // all loads in flight before the first MFMA
@@ -2559,8 +2586,6 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // FULL launches of a fixed shape: the G tiles of a wave are known at compile time; their operator
     // fragments are loaded with the partial sums and their MFMAs interleave with the F tiles' (same
     // accumulation order per tile as the general form below)
-    constexpr int kMTG = S::NK / 16, kGT = (kMTG + MAXT / 64 - 1) / (MAXT / 64);
-    constexpr bool kS2Fix = FULL && S::kNW > 0;
     constexpr bool kS2Batch = kS2Fix && kLatS;  // stage 2's partial sums read in one batch
     // WF: the F tiles (dP, with the residual z folded in), WG: the G tiles (Gb).  The GD flows run both in
     // one pass; the BLS flow runs G in the rounds with a new gradient input and F in every trial round
@@ -2577,8 +2602,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 const int u = nwaves - 1 - wave + g * nwaves;
                 ga[g][0] = ga[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
                 if (u < kMTG) {
-                    ga[g][0] = vn_frag(u * KQ2);
-                    ga[g][1] = vn_frag(u * KQ2 + 1);
+                    ga[g][0] = kVReg ? vnR[g][0] : vn_frag(u * KQ2);
+                    ga[g][1] = kVReg ? vnR[g][1] : vn_frag(u * KQ2 + 1);
                 }
             }
         }
@@ -2722,6 +2747,23 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     float* Ajb = smem + LX.aj;   // BLS: the round's trial iterate α_j, rows [column][waypoint]
     float* Zq = smem + LX.zp;    // BLS: z partials, quad-major
     float* TS = smem + LX.ts;    // BLS: per-slot lr, ‖G‖, in-a-line-search flag
+    // V_R staged in LDS: the G-tile waves' V_R / V_Rᵀ fragments held in VGPRs for the launch (as kVReg)
+    constexpr int kTB = kBFix ? (S::NK / 16 + MAXT / 64 - 1) / (MAXT / 64) : 1;  // tiles per wave
+    // (C3-BLS faithful 7.21 -> 7.17 ms, C3-BLS 1.426 -> 1.419 ms; bit-identical)
+    constexpr bool kVRegB = BLS && VL && kBFix;
+    f32x4 bvt[kVRegB ? kTB : 1], bvn[kVRegB ? kTB : 1][2];
+    if constexpr (kVRegB) {
+#pragma unroll
+        for (int g = 0; g < kTB; ++g) {
+            const int u = nwaves - 1 - wave + g * (MAXT / 64);
+            bvt[g] = bvn[g][0] = bvn[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+            if (u < S::NK / 16) {
+                bvt[g] = vt_frag(u);
+                bvn[g][0] = vn_frag(u * KQ2);
+                bvn[g][1] = vn_frag(u * KQ2 + 1);
+            }
+        }
+    }
     auto bls_gz = [&](auto freshc, bool hmr, int hsr) {  // fresh (a new direction this round): G from y''
         constexpr bool fresh = decltype(freshc)::value;
         const int pz = nwaves - 1 - wave;  // this wave's z partial; its G tiles are u = pz + g·nwaves
@@ -2743,7 +2785,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 Ap[g] = Vp[g] = Gt[g] = f32x4{0.f, 0.f, 0.f, 0.f};
                 if (u < S::NK / 16) {
                     Ap[g] = *reinterpret_cast<const f32x4*>(Ab + ycl * lde + u * 16 + r4y);
-                    Vp[g] = vt_frag(u);
+                    Vp[g] = kVRegB ? bvt[g] : vt_frag(u);
                     if constexpr (!fresh) Gt[g] = *reinterpret_cast<const f32x4*>(Gb + ycl * lde + u * 16 + r4y);
                 }
             }
@@ -2764,8 +2806,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     const int u = pz + g * (MAXT / 64);
                     gv[g][0] = gv[g][1] = f32x4{0.f, 0.f, 0.f, 0.f};
                     if (u < S::NK / 16) {
-                        gv[g][0] = vn_frag(u * KQ2);
-                        gv[g][1] = vn_frag(u * KQ2 + 1);
+                        gv[g][0] = kVRegB ? bvn[g][0] : vn_frag(u * KQ2);
+                        gv[g][1] = kVRegB ? bvn[g][1] : vn_frag(u * KQ2 + 1);
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
@@ -3197,6 +3239,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     for (int par = 0;; par ^= 1) {
         f32x4 pre1[KQU1], pre1w[KQU1];
         float pre1e = 0.f;  // read only on the endpoint waves (hasep)
+        // (the flag word read before the operand batch, so the branch need not wait for the batch: C3 even
+        // to 2 % slower, not kept)
         if constexpr (kPre1) stage1_load(pre1, pre1w, pre1e);
         const unsigned fl = fw[par];
         if constexpr (GD1) {
