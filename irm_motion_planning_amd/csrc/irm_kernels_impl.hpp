@@ -2514,15 +2514,12 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     constexpr int kKQZ = kZFix ? kKQa / kZS : 1;
     constexpr int kMTG = S::NK / 16, kGT = (kMTG + MAXT / 64 - 1) / (MAXT / 64);
     constexpr bool kS2Fix = FULL && S::kNW > 0;
-    // V_R staged in LDS (C3's shape), GD flows: the z unit's V_Rᵀ fragments and the G tiles' V_R fragments
-    // are the same every round — held in VGPRs for the launch instead of re-read from LDS each round
-    // (C3 faithful 3.93 -> 3.75 ms, C3 even; bit-identical)
-#ifdef IRM_X_VREGL2
-    // (from L2 too; not the 7-DoF N = 256 dual loop / 256-thread variants, which spill with them)
+    // GD flows of the fixed shapes: the z unit's V_Rᵀ fragments and the G tiles' V_R fragments are the same
+    // every round — held in VGPRs for the launch instead of re-read from LDS / L2 each round
+    // (C3 faithful 3.93 -> 3.75 ms, C3 even; from L2 too: C7 1.33 -> 1.27 ms, C7 faithful 7.52 -> 7.30 ms,
+    // C5 1.405 -> 1.326 ms, C4 even; bit-identical.  Not the 7-DoF N = 256 dual loop / 256-thread
+    // variants, which spill with them)
     constexpr bool kVReg = !BLS && !DENSE && kZFix && kS2Fix && (VL || !(D > 3 && S::NK > 128) || (GD1 && MAXT > 256));
-#else
-    constexpr bool kVReg = !BLS && !DENSE && VL && kZFix && kS2Fix;
-#endif
     f32x4 vtR[kVReg ? kKQZ : 1], vnR[kVReg ? kGT : 1][2];
     if constexpr (kVReg) {
         const int sp = nwaves - 1 - wave;
@@ -2638,6 +2635,44 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             for (int sp = 1; sp < NS; ++sp) {
                 by[0] += yp[sp];
                 b1 += f32x2{yq[sp].x, yq[sp].y};
+            }
+            if constexpr (kS2Fix && WF && WG) {
+                // the G tiles first, on y'' alone (read first), while the z partials are still in flight;
+                // then the F tiles on y'' + z — each tile's MFMA chain unchanged (bit-identical; C3 −0.4 %,
+                // C3 faithful −1 %)
+                const f32x4 by1 = f32x4{b1.x, b1.y, 0.f, 0.f};
+                f32x4 ag[kGT];
+#pragma unroll
+                for (int g = 0; g < kGT; ++g) {
+                    ag[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    if (nwaves - 1 - wave + g * nwaves < kMTG) {
+#pragma unroll
+                        for (int m = 0; m < 4; ++m) ag[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(ga[g][0][m], by[0][m], ag[g], 0, 0, 0);
+#pragma unroll
+                        for (int m = 0; m < 2; ++m) ag[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(ga[g][1][m], by1[m], ag[g], 0, 0, 0);
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);  // (the z sums after the G chain: it must not wait for them)
+                f32x4 bz = zq[0];
+#pragma unroll
+                for (int sp = 1; sp < kZS; ++sp) bz += zq[sp];
+                const f32x4 b0 = by[0] + bz;
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+#pragma unroll
+                    for (int j = 0; j < S2T; ++j)
+                        if (wave + j * nwaves < MT2)
+                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a2[j * 2][m], b0[m], acc[j], 0, 0, 0);
+#pragma unroll
+                for (int j = 0; j < S2T; ++j)
+                    if (wave + j * nwaves < MT2)
+                        *reinterpret_cast<f32x4*>(dP + cl * ldx + (wave + j * nwaves) * 16 + r4x) = acc[j];
+#pragma unroll
+                for (int g = 0; g < kGT; ++g) {
+                    const int u = nwaves - 1 - wave + g * nwaves;
+                    if (u < kMTG) *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4x) = ag[g];
+                }
+                return;
             }
             if constexpr (WF) {
                 f32x4 bz = zq[0];
