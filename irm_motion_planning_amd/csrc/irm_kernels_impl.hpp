@@ -2221,10 +2221,12 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     const float* obs = obsL + (P.obs_stride ? t * obs_pitch(P.O) : 0);  // (a helper round: t*'s)
     // 9-12 obstacles (the reference's 11): the padded table in VGPRs for the whole launch (24 floats),
     // so the per-round evaluation does not wait on its LDS reads
-#ifndef IRM_X_OREG_ALL
-    constexpr bool OREG = GD1;
-#else
+    // (and the 3-joint GD dual loop: C3 faithful 3.70 -> 3.60 ms; the BLS flow with it measured C3-BLS
+    // −0.5 % but C2 +2.7 %, not used; the 7-DoF dual loop spills with it)
+#if defined(IRM_X_OREG_ALL)
     constexpr bool OREG = true;
+#else
+    constexpr bool OREG = GD1 || (D <= 3 && !BLS);
 #endif
     f32x4 oreg[OREG ? 6 : 1];
     const bool obs_reg = ((P.O + 3) >> 2) == 3;
@@ -3326,6 +3328,12 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 for (int k = 0; k < D; ++k) tg[0][k] = (nn[0] == N - 1) ? P.goal[bs * D + k] : P.start[bs * D + k];
                 vl[0] = wl[0];
                 obs = obsL + (P.obs_stride ? ts * obs_pitch(P.O) : 0);  // t*'s obstacles (per-problem sets)
+                if constexpr (OREG) {  // (the register copy of the table too)
+                    if (P.obs_stride && obs_reg) {
+#pragma unroll
+                        for (int i = 0; i < 6; ++i) oreg[i] = reinterpret_cast<const f32x4*>(obs)[i];
+                    }
+                }
                 h_lr0 = HP[ts * kHpW + 0];
                 h_lr = h_lr0 * P.bls_bm;
                 h_ljl = HP[ts * kHpW + 1];

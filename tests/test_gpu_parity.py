@@ -979,6 +979,29 @@ def test_bls_line_search_helpers_change_nothing(cfg, monkeypatch):
     print(f"{cfg}: {int(st0['bls_trials'].sum())} trials, log of problem 0: {len(tr0)} rows, identical")
 
 
+def test_bls_helpers_with_distinct_per_problem_obstacles(monkeypatch):
+    """A helper evaluates t*'s trial against t*'s obstacle set: with per-problem tables (each problem its
+    own 11 obstacles, so a helper's own table is the wrong one) helpers on and off must still give
+    bit-identical α, trajectories, statistics and line-search log (the kernel's register copy of the table
+    is reloaded from t*'s when a slot starts helping)."""
+    import bench
+    s, g, obs = bench.make_problem("c3bls", 1, 0)
+    B = 64
+    s, g = s[:B], g[:B]
+    rng = np.random.default_rng(23)
+    per = (obs[None, :, :] + rng.uniform(-0.3, 0.3, (B,) + obs.shape)).astype(np.float32)
+    outs = []
+    for off in ("1", "0"):
+        monkeypatch.setenv("IRM_LEAN_NOHELP", off)
+        c = _flow_ctx("c3bls", 4, True)
+        c.bls_trace_enable(4096)
+        a, t, st = c.optimize(s, g, per, obstacle_stride=2 * obs.shape[0])
+        outs.append((a, t, st, c.bls_trace(int(st["bls_trials"][0]))))
+    (a0, t0, st0, tr0), (a1, t1, st1, tr1) = outs
+    _assert_same((a1, t1, st1), (a0, t0, st0), "per-problem obstacles: helpers on vs off")
+    np.testing.assert_array_equal(tr1, tr0)
+
+
 def test_bls_helpers_with_five_trajectories_per_workgroup(monkeypatch):
     """N = 64 BLS at five 3-joint trajectories per workgroup (15 of the 16 MFMA columns): when slot 4 is the
     last live trajectory, its helper must be a slot whose columns exist (slot 5 would own columns 15-17).
