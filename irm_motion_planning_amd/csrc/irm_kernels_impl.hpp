@@ -2195,6 +2195,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
     for (int j = 0; j < WPL; ++j) {
         epf[j] = (nn[j] == 0 || nn[j] == N - 1) ? 1.f : 0.f;
+        // opaque to the compiler: tests of epf stay one compare (it otherwise re-derives the nested
+        // n == 0 / n == N − 1 tests from the select, an exec-mask cascade of ≈ 20 scalar instructions)
+        asm volatile("" : "+v"(epf[j]));
         endm[j] = __ballot(epf[j] != 0.f);
 #pragma unroll
         for (int k = 0; k < D; ++k) tg[j][k] = (nn[j] == N - 1) ? g[k] : s[k];
@@ -2281,7 +2284,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
         for (int j = 0; j < WPL; ++j) {
             const int n = nn[j];
-            if (lv[j] && (n == 0 || n == N - 1)) {  // trajectory.py:183-204 rows 0 and N−1
+            if (lv[j] && epf[j] != 0.f) {  // trajectory.py:183-204 rows 0 and N−1 (epf: one compare, no cascade)
                 float a = 0.f, bb = 0.f;
 #pragma unroll
                 for (int d = 0; d < D; ++d) {
@@ -2351,7 +2354,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         for (int ww = 1; ww < WPTL; ++ww) {
             const float ov = rr[ww][0];
             const int oi = __float_as_int(rr[ww][1]);
-            const bool take = ov > cmax || (ov == cmax && oi < cidx);  // amax_step
+            const bool take = (ov > cmax) | ((ov == cmax) & (oi < cidx));  // amax_step (no short-circuit branch)
             cmax = take ? ov : cmax;
             cidx = take ? oi : cidx;
             usum += rr[ww][2];
@@ -2403,12 +2406,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     ep[k] = mb;
                 }
                 if (endrow) {  // the compact copy of the endpoint rows (read at the next round's top)
-                    if (n == 0)
+                    // (one region with a per-lane address: the nested n == 0 / n == N − 1 tests compiled to
+                    // an exec-mask cascade of ≈ 20 scalar instructions on every wave)
+                    float* e = EPg + (n == 0 ? 0 : kEpS);
 #pragma unroll
-                        for (int k = 0; k < D; ++k) EPg[k] = ep[k];
-                    if (n == N - 1)
-#pragma unroll
-                        for (int k = 0; k < D; ++k) EPg[kEpS + k] = ep[k];
+                    for (int k = 0; k < D; ++k) e[k] = ep[k];
                 }
             }
         }

@@ -54,7 +54,7 @@ for b in blocks:
         loops[b[1]].append(b)
 hdr = max(loops, key=lambda k: len(loops[k]))
 lb = loops[hdr]
-latch = max(i for i, b in enumerate(lb) if (".L" + hdr) in b[4])
+latch = max((i for i, b in enumerate(lb) if (".L" + hdr) in b[4]), default=len(lb) - 1)  # (fall-through back edge: the last block)
 hot = [b for i, b in enumerate(lb) if i <= latch and not b[2]]
 cold = [b for i, b in enumerate(lb) if not (i <= latch and not b[2])]
 
