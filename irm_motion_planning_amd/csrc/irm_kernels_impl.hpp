@@ -3468,6 +3468,15 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         // ------------------------------------------------ update + evaluate
         float q2[WPL][D], v2[WPL][D];
         WP<D> w[WPL];
+        // the GD single loop's G rows of the α update read with the direction (stage 2 wrote both), so their
+        // LDS round trip is off the decision's path: C3 −1.3 %; the dual loop, C5 and C7 measured 0.8-1 %
+        // slower with it (bit-identical either way)
+#ifdef IRM_X_GPRE
+        constexpr bool kGPre = !BLS;
+#else
+        constexpr bool kGPre = GD1 && D <= 3;
+#endif
+        float Gp[kGPre ? WPL : 1][D];
         const bool stepping = GD1 ? !done : (phase == LP_STEP || helper);  // wave-uniform
         const bool ev = GD1 ? !done : (phase != LP_DONE || helper);
         if (ev) {
@@ -3477,6 +3486,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     float dt[D], dv[D];
                     {
                         direction(j, dt, dv);
+                        if constexpr (kGPre) grad_alpha(j, Gp[j], t);
 #pragma unroll
                         for (int k = 0; k < D; ++k) {
                             const float tq = -(stepj * dt[k]), tv = -(stepj * dv[k]);
@@ -3693,7 +3703,12 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
                 for (int j = 0; j < WPL; ++j) {
                     float G[D];
-                    grad_alpha(j, G, t);
+                    if constexpr (kGPre) {
+#pragma unroll
+                        for (int k = 0; k < D; ++k) G[k] = Gp[j][k];
+                    } else {
+                        grad_alpha(j, G, t);
+                    }
                     // the D element chains first (one basic block, interleaved), then the residual stores
                     float eo[D];
 #pragma unroll
