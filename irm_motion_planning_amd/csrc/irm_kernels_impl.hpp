@@ -3192,6 +3192,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // round 0 (optimizer_GD.py:93 / :210: the loss at α0) and the first gradient inputs
     irm_stats st{};
     st.series_len = rec ? 1 : 0;
+    // BLS: the per-trajectory counters in VGPRs (the compiler would keep these wave-uniform values in SGPRs,
+    // and the BLS flow's scalar state spills SGPRs to VGPR lanes — readlane / writelane on the round's path):
+    // C3-BLS −0.9 %, its faithful line −0.4 %, C2 −0.7 %; the GD dual loop 1-1.6 % slower with it, not used
+    if constexpr (BLS) {
+        asm volatile("" : "+v"(st.inner_iterations), "+v"(st.outer_iterations), "+v"(st.grad_evals), "+v"(st.cost_evals),
+                     "+v"(st.bls_trials), "+v"(st.series_len), "+v"(n_rounds), "+v"(n_hm));
+    }
     auto write_out = [&]() {  // this trajectory's outputs: T, α, counters
 #pragma unroll
         for (int j = 0; j < WPL; ++j) {
