@@ -2889,9 +2889,32 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             const float s2 = __uint_as_float(p16[0]) + __uint_as_float(p16[1]);
             const auto p32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(s2), __float_as_uint(s2), false, false);
             const int cs = __float_as_int(__uint_as_float(p32[0]) + __uint_as_float(p32[1]));
-            float g2 = __int_as_float(__builtin_amdgcn_ds_bpermute((sc * D) << 2, cs));
+            float g2;
+            if constexpr (D <= 3) {
+                // the slot's D column sums by in-row shifts (the slot's columns sit in this lane's row; a
+                // helper's own columns hold t*'s sums, from the same y'' columns): same adds in the same order
+                // as the gather below, without its LDS round trips
+                const int o = cl % D;
+                const float c0 = __int_as_float(cs);
+                const float r1 = __int_as_float(__builtin_amdgcn_mov_dpp(cs, 0x111, 0xF, 0xF, true));  // row_shr:1
+                const float l1 = __int_as_float(__builtin_amdgcn_mov_dpp(cs, 0x101, 0xF, 0xF, true));  // row_shl:1
+                if constexpr (D == 1) {
+                    g2 = c0;
+                } else if constexpr (D == 2) {
+                    g2 = (o == 0 ? c0 : r1) + (o == 0 ? l1 : c0);
+                } else {
+                    const float r2 = __int_as_float(__builtin_amdgcn_mov_dpp(cs, 0x112, 0xF, 0xF, true));  // row_shr:2
+                    const float l2 = __int_as_float(__builtin_amdgcn_mov_dpp(cs, 0x102, 0xF, 0xF, true));  // row_shl:2
+                    const float a0 = o == 0 ? c0 : (o == 1 ? r1 : r2);
+                    const float a1 = o == 0 ? l1 : (o == 1 ? c0 : r1);
+                    const float a2 = o == 0 ? l2 : (o == 1 ? l1 : c0);
+                    g2 = (a0 + a1) + a2;
+                }
+            } else {
+                g2 = __int_as_float(__builtin_amdgcn_ds_bpermute((sc * D) << 2, cs));
 #pragma unroll
-            for (int a = 1; a < D; ++a) g2 += __int_as_float(__builtin_amdgcn_ds_bpermute((sc * D + a) << 2, cs));
+                for (int a = 1; a < D; ++a) g2 += __int_as_float(__builtin_amdgcn_ds_bpermute((sc * D + a) << 2, cs));
+            }
             gn = __builtin_amdgcn_sqrtf(g2);  // v_sqrt_f32 (≤ 1 ulp): every user reads this value (TS)
             if (pz == 0 && lane < kCols && ycl == cl && cl % D == 0) TS[(cl / D) * kTsW + 1] = gn;  // for the trajectories and the later rounds
             if constexpr (!kBFix) {
@@ -3484,6 +3507,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         constexpr bool kGPre = GD1 && D <= 3;
 #endif
         float Gp[kGPre ? WPL : 1][D];
+        // BLS: this slot's trial iterate α_j read with the direction (bls_gz wrote it), off the accept's path
+        constexpr bool kAjPre = BLS;
+        float Ajp[kAjPre ? WPL : 1][D];
         const bool stepping = GD1 ? !done : (phase == LP_STEP || helper);  // wave-uniform
         const bool ev = GD1 ? !done : (phase != LP_DONE || helper);
         if (ev) {
@@ -3494,6 +3520,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     {
                         direction(j, dt, dv);
                         if constexpr (kGPre) grad_alpha(j, Gp[j], t);
+                        if constexpr (kAjPre) {
+#pragma unroll
+                            for (int k = 0; k < D; ++k) Ajp[j][k] = Ajb[(t * D + k) * lde + swz(wl[j] ? nn[j] : 0, t * D + k)];
+                        }
 #pragma unroll
                         for (int k = 0; k < D; ++k) {
                             const float tq = -(stepj * dt[k]), tv = -(stepj * dv[k]);
@@ -3551,7 +3581,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                         float ajh[WPL][D];
 #pragma unroll
                         for (int k = 0; k < D; ++k) {
-                            ajh[0][k] = Ajb[(t * D + k) * lde + swz(nn[0], t * D + k)];
+                            ajh[0][k] = kAjPre ? Ajp[0][k] : Ajb[(t * D + k) * lde + swz(nn[0], t * D + k)];
                             if (wl[0]) Ab[(ts * D + k) * lde + swz(nn[0], ts * D + k)] = ajh[0][k];
                         }
                         ss_write(ts, ajh, q2, v2);
@@ -3697,7 +3727,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     for (int k = 0; k < D; ++k) {
                         const int o = (t * D + k) * lde + swz(wl[j] ? nn[j] : 0, t * D + k);
                         if (wl[j]) {
-                            al[j][k] = Ajb[o];
+                            al[j][k] = kAjPre ? Ajp[j][k] : Ajb[o];
                             Ab[o] = al[j][k];
                         }
                         q[j][k] = q2[j][k];

@@ -1,5 +1,8 @@
 """Developer diagnostic: per-phase cycle breakdown of k_optimize.
 
+IRM_PROF_FIRST=<problem> moves that problem to batch slot 0 (the stamping wave is then its own) and,
+with "cfg!f", reports block 0.
+
 Needs the IRM_PHASE_PROFILE build (python -m irm_motion_planning_amd.build --prof);
 run with IRM_LIB=<repo>/irm_motion_planning_amd/libirm_hip_prof.so on the GPU box.
 """
@@ -34,6 +37,11 @@ def run(cfg, tb=0, rank=0, faithful=False):
         os.environ["IRM_TRACE_PROBLEM"] = str(1 << 29)
     args = bench.make_args(cfg, faithful, 200)
     start, goal, obstacles = bench.make_problem(cfg, 1, 0)
+    first = os.environ.get("IRM_PROF_FIRST")  # problem index moved to batch slot 0: its own waves stamp
+    if first:
+        idx = np.arange(start.shape[0])
+        idx[0], idx[int(first)] = int(first), 0
+        start, goal = start[idx], goal[idx]
     ctx = Context(params_from_args(args, traj_per_block=tb, operator_rank=rank))
     info = ctx.info()
     ctx.optimize(start, goal, obstacles)
@@ -58,7 +66,7 @@ def run(cfg, tb=0, rank=0, faithful=False):
         elif c > 0:
             print(f"   {name:22s} {c/rounds:9.0f} cyc/round  ({100*c/tot.mean():5.1f} %)")
     if faithful:  # the block that bounds the launch: its own rounds (its slowest problem's kernel rounds)
-        k = int(np.argmax(tot))
+        k = 0 if first else int(np.argmax(tot))
         tbk = info["traj_per_block"]
         kr = (st["series_len"][k * tbk:(k + 1) * tbk] & 0xFFFF).max() if args.optimizer_name == "bls" else 0
         kr = float(kr) if kr > 0 else rounds
