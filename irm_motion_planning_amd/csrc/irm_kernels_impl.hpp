@@ -809,6 +809,9 @@ __device__ __forceinline__ void eval_exact_loop(const KParams& P, const float* _
     }
 #pragma unroll
     for (int k = 0; k < D; ++k) {
+        // one column of J at a time: without the barrier the scheduler hoists all D² LDS reads and their fp64
+        // conversions (2·D² = 98 VGPRs at D = 7) ahead of the first product — the resync's register peak
+        __builtin_amdgcn_sched_barrier(0);
         double sq = 0.0, sv = 0.0;
 #pragma unroll
         for (int d = 0; d < D; ++d) {
@@ -2118,6 +2121,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // banks) are then both conflict-free; per-row accesses stay so (a column's rows only permute).
     const int r4x = r4 ^ (cl & 4);
     auto swz = [](int r, int c) { return r ^ (c & 4); };
+    // 7-DoF shapes: a lane index laundered at a rare path's use, so that the path's per-lane addresses are
+    // formed there instead of being held across the round loop (the 7-DoF dual-loop / BLS variants spilled
+    // them); the 3-joint shapes have the registers, and measured 3 % slower on C3-BLS with it
+    auto lnd = [](int x) {
+        if constexpr (D > 3) asm volatile("" : "+v"(x));
+        return x;
+    };
     int ycl = cl;     // stage 2's Ypart column for this lane's B column (a helper round: the helper's read t*'s)
     int r4y = r4x;    // its first row under the row swizzle of column ycl
     const bool has1 = wave < MT1 * nsplit;
@@ -2127,25 +2137,52 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // ----------------------------------------------------------- prologue
     f32x4 a1[S1Q], a1v[RV ? S1Q : 1], a2[S2T * 2];
     auto load_ops = [&]() {
-        const f32x4* g1 = reinterpret_cast<const f32x4*>(P.F1p);
-        const f32x4* g2 = reinterpret_cast<const f32x4*>(P.F2p);
+        if constexpr (!VL) {  // (the shapes whose operands are read from L2: N = 256, 7-DoF, 256-thread)
+            // buffer loads (the lane's offset in one VGPR): this also runs after each 7-DoF resync
+            // (kReloadOps), where per-load 64-bit addresses held across the round loop were spilled
+            const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<float*>(P.F1p), 0, (int)(frag_floats(RP, MP) * 4), 0x00020000);
+            const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<float*>(P.F2p), 0, (int)(frag_floats(MP, RP) * 4), 0x00020000);
+            const int vo = lane * 16;
 #pragma unroll
-        for (int i = 0; i < S1Q; ++i) {
-            a1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-            if (has1 && kq0 + i < kq1) a1[i] = g1[((size_t)tile1 * KQ1 + kq0 + i) * 64 + lane];
-            if constexpr (RV) {
-                a1v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-                if (has1 && kq0 + i < kq1) a1v[i] = g1[((size_t)tile1 * KQ1 + KQa + kq0 + i) * 64 + lane];
+            for (int i = 0; i < S1Q; ++i) {
+                a1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (has1 && kq0 + i < kq1) a1[i] = ld_frag(r1, vo, ((tile1 * KQ1 + kq0 + i) * 64) * 16);
+                if constexpr (RV) {
+                    a1v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    if (has1 && kq0 + i < kq1) a1v[i] = ld_frag(r1, vo, ((tile1 * KQ1 + KQa + kq0 + i) * 64) * 16);
+                }
             }
+#pragma unroll
+            for (int j = 0; j < S2T; ++j)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    a2[j * 2 + i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    const int tile = wave + j * nwaves;
+                    if (tile < MT2 && i < KQ2) a2[j * 2 + i] = ld_frag(r2, vo, ((tile * KQ2 + i) * 64) * 16);
+                }
+        } else {
+            const f32x4* g1 = reinterpret_cast<const f32x4*>(P.F1p);
+            const f32x4* g2 = reinterpret_cast<const f32x4*>(P.F2p);
+#pragma unroll
+            for (int i = 0; i < S1Q; ++i) {
+                a1[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (has1 && kq0 + i < kq1) a1[i] = g1[((size_t)tile1 * KQ1 + kq0 + i) * 64 + lane];
+                if constexpr (RV) {
+                    a1v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    if (has1 && kq0 + i < kq1) a1v[i] = g1[((size_t)tile1 * KQ1 + KQa + kq0 + i) * 64 + lane];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < S2T; ++j)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    a2[j * 2 + i] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    const int tile = wave + j * nwaves;
+                    if (tile < MT2 && i < KQ2) a2[j * 2 + i] = g2[((size_t)tile * KQ2 + i) * 64 + lane];
+                }
         }
-#pragma unroll
-        for (int j = 0; j < S2T; ++j)
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                a2[j * 2 + i] = f32x4{0.f, 0.f, 0.f, 0.f};
-                const int tile = wave + j * nwaves;
-                if (tile < MT2 && i < KQ2) a2[j * 2 + i] = g2[((size_t)tile * KQ2 + i) * 64 + lane];
-            }
     };
     if constexpr (!DENSE) load_ops();  // (DENSE: every operator fragment streamed from L2 in its stage)
     // The endpoint velocity rows b'[0], b'[N−1] (stage 1's operator Fᵀ has zero columns there, so that a
@@ -2160,6 +2197,17 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     if (hasep && (lane >> 4) < 2) aep = P.Fbot[(size_t)((lane >> 4) ? N - 1 : 0) * RP + tile1 * 16 + (lane & 15)];
     // this lane's B address: column cl of trajectory cl / D, row k = lane >> 4 (a zero slot for k ≥ 2)
     const int epoff = (lane >> 4) < 2 ? LX.ep + (cl / D) * 2 * kEpS + (lane >> 4) * kEpS + cl % D : LX.ep0;
+    // the 7-DoF BLS flow forms it again at its use (held across the round loop it was spilled)
+    auto ep_at = [&]() {
+        if constexpr (BLS && D > 3 && MAXT > 256) {
+            int l = lane;
+            asm volatile("" : "+v"(l));
+            const int c = l & 15;
+            return (l >> 4) < 2 ? LX.ep + (c / D) * 2 * kEpS + (l >> 4) * kEpS + c % D : LX.ep0;
+        } else {
+            return epoff;
+        }
+    };
     if constexpr (VL) {
         const int nv = (int)frag_floats(RP, NK) / 4;  // = frag_floats(NK, RP) / 4
         const f32x4* gt = reinterpret_cast<const f32x4*>(P.VTp);
@@ -2408,7 +2456,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 if (endrow) {  // the compact copy of the endpoint rows (read at the next round's top)
                     // (one region with a per-lane address: the nested n == 0 / n == N − 1 tests compiled to
                     // an exec-mask cascade of ≈ 20 scalar instructions on every wave)
-                    float* e = EPg + (n == 0 ? 0 : kEpS);
+                    const int n2 = lnd(n);  // (7-DoF: the offset formed here, not held across the round loop)
+                    float* e = EPg + (n2 == 0 ? 0 : kEpS);
 #pragma unroll
                     for (int k = 0; k < D; ++k) e[k] = ep[k];
                 }
@@ -2464,13 +2513,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         // zero itself (one MFMA result either way: no zeroed accumulator on the non-endpoint waves)
         if constexpr (kFix) {
             if (hasep) {
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(aep, kPre1 ? prep : smem[epoff], z4, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(aep, kPre1 ? prep : smem[ep_at()], z4, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[0][1], bv[0][1], acc1, 0, 0, 0);
             } else {
                 acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[0][1], bv[0][1], z4, 0, 0, 0);
             }
         } else if (hasep) {
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(aep, kPre1 ? prep : smem[epoff], acc1, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(aep, kPre1 ? prep : smem[ep_at()], acc1, 0, 0, 0);
         }
 #pragma unroll
         for (int i = 0; i < KQU; ++i) {
@@ -2491,6 +2540,18 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                         acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1v[i][2], bw[i][2], acc0, 0, 0, 0);
                         acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1v[i][3], bw[i][3], acc1, 0, 0, 0);
                     }
+                }
+            } else if constexpr (!VL) {
+                // (buffer loads: the lane's offset in one VGPR, no 64-bit address held across the round loop)
+                const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<float*>(P.F1p), 0, (int)(frag_floats(RP, MP) * 4), 0x00020000);
+                for (int kq = kq0; kq < kq1; ++kq) {
+                    const f32x4 a = ld_frag(r1, lane * 16, ((tile1 * KQ1 + KQa + kq) * 64) * 16);
+                    const f32x4 bb = *reinterpret_cast<const f32x4*>(xl + (KQa + kq) * 16);
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], bb[0], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], bb[1], acc1, 0, 0, 0);
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], bb[2], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], bb[3], acc1, 0, 0, 0);
                 }
             } else {
                 const f32x4* ap = reinterpret_cast<const f32x4*>(P.F1p) + ((size_t)tile1 * KQ1 + KQa) * 64 + lane;
@@ -3159,6 +3220,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             else G[k] = Gb[(gt * D + k) * lde + swz(r, gt * D + k)];
         }
     };
+    // a lane's row offset in a series frame, formed where it is used (a value held across the round loop
+    // is a per-lane 64-bit address the 7-DoF dual loop spilled)
+    auto ser_row = [&](int j) {
+        int r = nn[j] * D;
+        if constexpr (D > 3) asm volatile("" : "+v"(r));
+        return r;
+    };
     auto snapshot = [&](irm_stats& st) {  // extended-vis frame after a non-breaking inner iteration
         if (rec && st.series_len < P.max_series) {
 #pragma unroll
@@ -3166,7 +3234,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 if (vl[j]) {
 #pragma unroll
                     for (int k = 0; k < D; ++k)
-                        P.series[((b * P.max_series) + st.series_len) * N * D + nn[j] * D + k] = q[j][k];
+                        P.series[((b * P.max_series) + st.series_len) * N * D + ser_row(j) + k] = q[j][k];
                 }
             }
             st.series_len++;
@@ -3218,7 +3286,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // BLS: the per-trajectory counters in VGPRs (the compiler would keep these wave-uniform values in SGPRs,
     // and the BLS flow's scalar state spills SGPRs to VGPR lanes — readlane / writelane on the round's path):
     // C3-BLS −0.9 %, its faithful line −0.4 %, C2 −0.7 %; the GD dual loop 1-1.6 % slower with it, not used
-    if constexpr (BLS) {
+    if constexpr (BLS && D <= 3) {  // (the 7-DoF BLS variants have no VGPRs to spare)
         asm volatile("" : "+v"(st.inner_iterations), "+v"(st.outer_iterations), "+v"(st.grad_evals), "+v"(st.cost_evals),
                      "+v"(st.bls_trials), "+v"(st.series_len), "+v"(n_rounds), "+v"(n_hm));
     }
@@ -3415,10 +3483,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     float s1 = 0.f;
                     if (tvalid && li < RP) {
                         float sa = 0.f;
+                        const int lr = lnd(li);
 #pragma unroll
                         for (int a = 0; a < D; ++a) {
-                            float y = Ypart[(t * D + a) * ldy + swz(li, t * D + a)];
-                            for (int sp = 1; sp < nsplit; ++sp) y += Ypart[(sp * 16 + t * D + a) * ldy + swz(li, t * D + a)];
+                            float y = Ypart[(t * D + a) * ldy + swz(lr, t * D + a)];
+                            for (int sp = 1; sp < nsplit; ++sp) y += Ypart[(sp * 16 + t * D + a) * ldy + swz(lr, t * D + a)];
                             sa += y;
                         }
                         s1 = sa * sa;
@@ -3465,7 +3534,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     if (vl[j]) {
 #pragma unroll
                         for (int k = 0; k < D; ++k) {
-                            X[(t * D + k) * ldx + nn[j]] = al[j][k];
+                            X[(t * D + k) * ldx + lnd(nn[j])] = al[j][k];
                             if constexpr (!BLS) Eb[(t * D + k) * lde + swz(nn[j], t * D + k)] = 0.f;  // absorbed by the exact trajectory
                         }
                     }
@@ -3482,7 +3551,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                         if (rec && st.series_len > 0) {
 #pragma unroll
                             for (int k = 0; k < D; ++k)
-                                P.series[((b * P.max_series) + st.series_len - 1) * N * D + nn[j] * D + k] = q[j][k];
+                                P.series[((b * P.max_series) + st.series_len - 1) * N * D + ser_row(j) + k] = q[j][k];
                         }
                     }
                 }
@@ -3522,7 +3591,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                         if constexpr (kGPre) grad_alpha(j, Gp[j], t);
                         if constexpr (kAjPre) {
 #pragma unroll
-                            for (int k = 0; k < D; ++k) Ajp[j][k] = Ajb[(t * D + k) * lde + swz(wl[j] ? nn[j] : 0, t * D + k)];
+                            for (int k = 0; k < D; ++k) Ajp[j][k] = Ajb[(t * D + k) * lde + swz(wl[j] ? lnd(nn[j]) : 0, t * D + k)];
                         }
 #pragma unroll
                         for (int k = 0; k < D; ++k) {
@@ -3725,7 +3794,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 for (int j = 0; j < WPL; ++j)
 #pragma unroll
                     for (int k = 0; k < D; ++k) {
-                        const int o = (t * D + k) * lde + swz(wl[j] ? nn[j] : 0, t * D + k);
+                        const int o = (t * D + k) * lde + swz(wl[j] ? lnd(nn[j]) : 0, t * D + k);
                         if (wl[j]) {
                             al[j][k] = kAjPre ? Ajp[j][k] : Ajb[o];
                             Ab[o] = al[j][k];
