@@ -2585,6 +2585,10 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // C5 1.405 -> 1.326 ms, C4 even; bit-identical.  Not the 7-DoF N = 256 dual loop / 256-thread
     // variants, which spill with them)
     constexpr bool kVReg = !BLS && !DENSE && kZFix && kS2Fix && (VL || !(D > 3 && S::NK > 128) || (GD1 && MAXT > 256));
+    // otherwise (C5's dual loop) the z unit's V_Rᵀ fragments are loaded at the round's top, so their L2
+    // latency passes under stage 1 instead of holding the z waves at the stage-1 barrier
+    // (C5 faithful −1.4 %, C4 even; bit-identical)
+    constexpr bool kZPre = !BLS && !DENSE && kZFix && !kVReg;
     f32x4 vtR[kVReg ? kKQZ : 1], vnR[kVReg ? kGT : 1][2];
     if constexpr (kVReg) {
         const int sp = nwaves - 1 - wave;
@@ -2600,7 +2604,16 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             }
         }
     }
-    auto stage1z = [&]() {
+    auto zpre_load = [&](f32x4 (&zp)[kZPre ? kKQZ : 1]) {
+        if constexpr (kZPre) {
+            const int sp = nwaves - 1 - wave;
+            if (sp < kZS) {
+#pragma unroll
+                for (int i = 0; i < kKQZ; ++i) zp[i] = vt_frag(sp * kKQZ + i);
+            }
+        }
+    };
+    auto stage1z = [&](const f32x4 (&zp)[kZPre ? kKQZ : 1]) {
         const float* el = Eb + cl * lde + r4x;
         if constexpr (kZFix) {
             constexpr int KQZ = kKQZ;
@@ -2609,7 +2622,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             f32x4 a[KQZ], bb[KQZ];
 #pragma unroll
             for (int i = 0; i < KQZ; ++i) {
-                a[i] = kVReg ? vtR[i] : vt_frag(sp * KQZ + i);
+                if constexpr (kZPre) a[i] = zp[i];
+                else a[i] = kVReg ? vtR[i] : vt_frag(sp * KQZ + i);
                 bb[i] = *reinterpret_cast<const f32x4*>(el + (sp * KQZ + i) * 16);
             }
             if constexpr (kLatS) __builtin_amdgcn_sched_barrier(0);  // all loads in flight before the first MFMA
@@ -3375,6 +3389,8 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
     for (int par = 0;; par ^= 1) {
         f32x4 pre1[KQU1], pre1w[KQU1];
+        f32x4 zpre[kZPre ? kKQZ : 1];
+        zpre_load(zpre);
         float pre1e = 0.f;  // read only on the endpoint waves (hasep)
         // (the flag word read before the operand batch, so the branch need not wait for the batch: C3 even
         // to 2 % slower, not kept)
@@ -3453,7 +3469,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                     dense_stage1(dense);
                 } else {
                     stage1(dense, pre1, pre1w, pre1e);
-                    stage1z();
+                    stage1z(zpre);
                 }
                 IRM_STAMP(1);
                 __syncthreads();
