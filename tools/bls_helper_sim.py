@@ -5,7 +5,8 @@ Every problem of the bench batch is run through the C oracle's traced BLS dual l
 k_lean evaluates one trial of a trajectory plus one per helper slot (a finished neighbour evaluating the
 next trials lr·β, lr·β², ... — DESIGN.md §4), so an inner iteration with k trials takes ceil(k / (1 + h))
 rounds, plus one resync round per outer iteration.  The model assumes the trajectory is alone in its
-workgroup (helpers only serve a lone trajectory), so it bounds the rounds from below.
+workgroup (helpers only serve a lone trajectory), so it bounds the rounds from below; the per-workgroup
+simulation below plays the four problems of each workgroup together under several helper policies.
 
     python tools/bls_helper_sim.py [out.txt]
 """
@@ -47,6 +48,38 @@ def main():
         rounds = np.array([sum(int(np.ceil(c / (1 + h))) for c in cnt) + nout for _, cnt, nout in res])
         lines.append(f"helpers {h}: rounds per problem max {rounds.max()} p99 {np.percentile(rounds, 99):.0f} "
                      f"mean {rounds.mean():.0f}")
+    # per workgroup (four consecutive problems, as the faithful launch places them): each round every live
+    # trajectory runs one trial, plus its helpers' — "one": a done slot helps when exactly one is live (the
+    # kernel's policy); "multi": every done slot helps a lone trajectory; "pair": each live trajectory gets a
+    # done slot while there are enough
+    res.sort(key=lambda r: r[0])
+
+    def wg_rounds(wg, policy):
+        qs = [[list(cnt) + [1] * nout, 0, 0] for _, cnt, nout in wg]
+        rounds = 0
+        while True:
+            live = [i for i, q in enumerate(qs) if q[1] < len(q[0])]
+            if not live:
+                return rounds
+            done = len(qs) - len(live)
+            rounds += 1
+            for r, i in enumerate(live):
+                h = 0
+                if policy == "one" and len(live) == 1:
+                    h = 1
+                elif policy == "multi" and len(live) == 1:
+                    h = done
+                elif policy == "pair" and r < done:
+                    h = 1
+                q = qs[i]
+                q[2] += 1 + h
+                if q[2] >= q[0][q[1]]:
+                    q[1] += 1
+                    q[2] = 0
+    for policy in ("none", "one", "multi", "pair"):
+        wr = [wg_rounds(res[w * 4:(w + 1) * 4], policy) for w in range(len(res) // 4)]
+        lines.append(f"workgroups of four, helper policy {policy}: launch-bounding workgroup {max(wr)} rounds, "
+                     f"mean {np.mean(wr):.0f}")
     cnt = np.concatenate([c for _, c, _ in res])
     lines.append(f"trials per inner iteration, histogram 0..11: {np.bincount(cnt)[:12].tolist()}")
     b, c, nout = max(res, key=lambda r: r[1].sum())
