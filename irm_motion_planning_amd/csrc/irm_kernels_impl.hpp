@@ -2087,6 +2087,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     float* obsL = smem + H.obs;
     const int nsplit = sh.NSPLIT, zsplit = lean_zsplit(sh.NSPLIT, VL);
     constexpr bool kHelp = lean_help<S, MAXT, WPL, FULL, FLOW>();
+    // helpers read t*'s α, T, V from SS: t* publishes them at the top of each helper round rather than
+    // after every accepted trial of every trajectory (C3-BLS −1 %, its faithful line −0.6 %; bit-identical)
+    constexpr bool kSSLazy = kHelp;
     const LeanX LX = lean_extra(plan_lds(P, false, true, true).total, MP, NK, RP, nsplit, VL, D, kHelp ? MAXT : 0, BLS, DENSE);
     float* Eb = smem + LX.eb;  // e' rows [column][waypoint]
     float* Zp = smem + LX.zp;  // stage-1 partials of V_Rᵀ·e'
@@ -3349,7 +3352,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         }
         if constexpr (kHelp) {
             if (tvalid) {
-                ss_write(t, al, q, v);
+                if constexpr (!kSSLazy) ss_write(t, al, q, v);
                 if (n0 == 0 && lane == 0) {
                     HP[t * kHpW + 0] = lr;
                     HP[t * kHpW + 1] = ljl;
@@ -3437,8 +3440,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             }
             ycl = (hm && cl / D == hs) ? ts * D + cl % D : cl;
             r4y = r4 ^ (ycl & 4);
+            // t* publishes its α, T, V for the helper at the top of each helper round (the helper reads them
+            // after this round's G-tile barrier), instead of after every accepted trial of every trajectory
+            if constexpr (kSSLazy) {
+                if (hm && t == ts) ss_write(t, al, q, v);
+            }
             if (helper) {  // wave-uniform: t*'s state and scalars (its own trajectory is done and written out)
-                ss_read(ts);
+                if constexpr (!kSSLazy) ss_read(ts);
                 const size_t bs = (size_t)(tb0 + ts);
 #pragma unroll
                 for (int k = 0; k < D; ++k) tg[0][k] = (nn[0] == N - 1) ? P.goal[bs * D + k] : P.start[bs * D + k];
@@ -3515,6 +3523,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
             IRM_STAMP(3);
             __syncthreads();
             IRM_STAMP(4);
+            if constexpr (kSSLazy) {
+                if (helper) ss_read(ts);  // (t* wrote them at this round's top)
+            }
             bls_f();
             __syncthreads();
         }
@@ -3868,7 +3879,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 if constexpr (kHelp) {
                     // publish this trajectory's state for a helper: α, T, V when they changed (an accepted
                     // trial of its own, a new outer iteration's exact trajectory), the scalars every round
-                    if (phase == LP_STEP && (accept || rs)) ss_write(t, al, q, v);
+                    if (!kSSLazy && phase == LP_STEP && (accept || rs)) ss_write(t, al, q, v);
                     if (phase != LP_DONE && n0 == 0 && lane == 0) {
                         HP[t * kHpW + 0] = lr;
                         HP[t * kHpW + 1] = ljl;
