@@ -2669,6 +2669,14 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // WF: the F tiles (dP, with the residual z folded in), WG: the G tiles (Gb).  The GD flows run both in
     // one pass; the BLS flow runs G in the rounds with a new gradient input and F in every trial round
     // (its trial's own residual folded in, so the direction is the trial iterate's)
+    // the GD single loop's G tiles issued after the stage-2 barrier (their MFMAs under the update and
+    // evaluation; C3 -2.0 %, bit-identical)
+#ifdef IRM_X_GLATE_ALL
+    constexpr bool kGLate = !BLS && !DENSE && kS2Fix && kS2Batch;
+#else
+    constexpr bool kGLate = GD1 && D <= 3 && kS2Fix && kS2Batch;
+#endif
+    f32x4 glY0 = f32x4{0.f, 0.f, 0.f, 0.f}, glY1 = f32x4{0.f, 0.f, 0.f, 0.f};
     auto stage2f = [&](auto WFc, auto WGc) {
         constexpr bool WF = decltype(WFc)::value, WG = decltype(WGc)::value;
         f32x4 acc[S2T];
@@ -2724,10 +2732,14 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 // C3 faithful −1 %)
                 const f32x4 by1 = f32x4{b1.x, b1.y, 0.f, 0.f};
                 f32x4 ag[kGT];
+                if constexpr (kGLate) {
+                    glY0 = by[0];
+                    glY1 = by1;
+                }
 #pragma unroll
                 for (int g = 0; g < kGT; ++g) {
                     ag[g] = f32x4{0.f, 0.f, 0.f, 0.f};
-                    if (nwaves - 1 - wave + g * nwaves < kMTG) {
+                    if (!kGLate && nwaves - 1 - wave + g * nwaves < kMTG) {
 #pragma unroll
                         for (int m = 0; m < 4; ++m) ag[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(ga[g][0][m], by[0][m], ag[g], 0, 0, 0);
 #pragma unroll
@@ -2752,7 +2764,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
                 for (int g = 0; g < kGT; ++g) {
                     const int u = nwaves - 1 - wave + g * nwaves;
-                    if (u < kMTG) *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4x) = ag[g];
+                    if (!kGLate && u < kMTG) *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4x) = ag[g];
                 }
                 return;
             }
@@ -3493,6 +3505,24 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 IRM_STAMP(3);
                 __syncthreads();
                 IRM_STAMP(4);
+                if constexpr (kGLate) {
+                    // the G tiles after the stage-2 barrier: their MFMAs under the update / evaluation's VALU
+                    // work; Gb is read after the evaluation's barrier (the decision)
+#pragma unroll
+                    for (int g = 0; g < kGT; ++g) {
+                        const int u = nwaves - 1 - wave + g * nwaves;
+                        if (u < kMTG) {
+                            const f32x4 g0 = kVReg ? vnR[g][0] : vn_frag(u * KQ2);
+                            const f32x4 g1 = kVReg ? vnR[g][1] : vn_frag(u * KQ2 + 1);
+                            f32x4 ag = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                            for (int m = 0; m < 4; ++m) ag = __builtin_amdgcn_mfma_f32_16x16x4f32(g0[m], glY0[m], ag, 0, 0, 0);
+#pragma unroll
+                            for (int m = 0; m < 2; ++m) ag = __builtin_amdgcn_mfma_f32_16x16x4f32(g1[m], glY1[m], ag, 0, 0, 0);
+                            *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4x) = ag;
+                        }
+                    }
+                }
             }
         } else if ((fl >> 30) & 1u) {  // block-uniform: some trajectory has a line-search trial this round
             // (a round with a new direction: stage 1 first; the trial stages of bls_gz / bls_f, above)
@@ -3606,7 +3636,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #ifdef IRM_X_GPRE
         constexpr bool kGPre = !BLS;
 #else
-        constexpr bool kGPre = GD1 && D <= 3;
+        constexpr bool kGPre = GD1 && D <= 3 && !kGLate;
 #endif
         float Gp[kGPre ? WPL : 1][D];
         // BLS: this slot's trial iterate α_j read with the direction (bls_gz wrote it), off the accept's path
