@@ -2677,6 +2677,25 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     constexpr bool kGLate = GD1 && D <= 3 && kS2Fix && kS2Batch;
 #endif
     f32x4 glY0 = f32x4{0.f, 0.f, 0.f, 0.f}, glY1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    // (kGLate) the G tiles, issued right after the stage-2 barrier: their MFMAs under the update /
+    // evaluation's VALU work; Gb is read after the evaluation's barrier (the decision).  Issued after the
+    // update instead, C3 measured +5.7 %
+    auto glate_tiles = [&]() {
+#pragma unroll
+        for (int g = 0; g < kGT; ++g) {
+            const int u = nwaves - 1 - wave + g * nwaves;
+            if (u < kMTG) {
+                const f32x4 g0 = kVReg ? vnR[g][0] : vn_frag(u * KQ2);
+                const f32x4 g1 = kVReg ? vnR[g][1] : vn_frag(u * KQ2 + 1);
+                f32x4 ag = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int m = 0; m < 4; ++m) ag = __builtin_amdgcn_mfma_f32_16x16x4f32(g0[m], glY0[m], ag, 0, 0, 0);
+#pragma unroll
+                for (int m = 0; m < 2; ++m) ag = __builtin_amdgcn_mfma_f32_16x16x4f32(g1[m], glY1[m], ag, 0, 0, 0);
+                *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4x) = ag;
+            }
+        }
+    };
     auto stage2f = [&](auto WFc, auto WGc) {
         constexpr bool WF = decltype(WFc)::value, WG = decltype(WGc)::value;
         f32x4 acc[S2T];
@@ -3505,24 +3524,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 IRM_STAMP(3);
                 __syncthreads();
                 IRM_STAMP(4);
-                if constexpr (kGLate) {
-                    // the G tiles after the stage-2 barrier: their MFMAs under the update / evaluation's VALU
-                    // work; Gb is read after the evaluation's barrier (the decision)
-#pragma unroll
-                    for (int g = 0; g < kGT; ++g) {
-                        const int u = nwaves - 1 - wave + g * nwaves;
-                        if (u < kMTG) {
-                            const f32x4 g0 = kVReg ? vnR[g][0] : vn_frag(u * KQ2);
-                            const f32x4 g1 = kVReg ? vnR[g][1] : vn_frag(u * KQ2 + 1);
-                            f32x4 ag = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-                            for (int m = 0; m < 4; ++m) ag = __builtin_amdgcn_mfma_f32_16x16x4f32(g0[m], glY0[m], ag, 0, 0, 0);
-#pragma unroll
-                            for (int m = 0; m < 2; ++m) ag = __builtin_amdgcn_mfma_f32_16x16x4f32(g1[m], glY1[m], ag, 0, 0, 0);
-                            *reinterpret_cast<f32x4*>(Gb + cl * lde + u * 16 + r4x) = ag;
-                        }
-                    }
-                }
+                if constexpr (kGLate) glate_tiles();
             }
         } else if ((fl >> 30) & 1u) {  // block-uniform: some trajectory has a line-search trial this round
             // (a round with a new direction: stage 1 first; the trial stages of bls_gz / bls_f, above)
