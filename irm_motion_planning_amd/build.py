@@ -45,6 +45,8 @@ VARIANTS = {
     "defsched": ("libirm_hip_defsched.so", ["-DIRM_DEFAULT_SCHED"]),
     # the DynShape units with the iterative-ILP scheduler too (the D = 5 divergence check)
     "dynilp": ("libirm_hip_dynilp.so", ["-DIRM_DYN_ILP"]),
+    # the BLS trial stages count ĝ's mismatches against the IEEE division (tools/div_check.py)
+    "divchk": ("libirm_hip_divchk.so", ["-DIRM_DIV_CHECK"]),
 }
 
 
@@ -196,7 +198,7 @@ if __name__ == "__main__":
         sys.exit(0)
     build(force="--force" in sys.argv, verbose=True, jobs=jobs)
     for v in VARIANTS:  # e.g. --defsched (tools/sched_check.py)
-        if v and v != "prof" and f"--{v}" in sys.argv:
+        if v and v != "prof" and f"--{v}" in sys.argv:  # --defsched, --dynilp, --divchk
             build(force="--force" in sys.argv, variant=v, verbose=True, jobs=jobs)
     if "--prof" in sys.argv:
         build(force="--force" in sys.argv, variant="prof", verbose=True, jobs=jobs)

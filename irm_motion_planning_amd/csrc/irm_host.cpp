@@ -910,7 +910,7 @@ int irm_debug_bls_trace(irm_ctx* c, float* out, int32_t cap) {
 
 int irm_debug_phase_profile(irm_ctx* c, uint64_t* out, int32_t max_blocks) {
     if (!c || !out) return fail(IRM_EINVAL, "null argument");
-#ifdef IRM_PHASE_PROFILE
+#if defined(IRM_PHASE_PROFILE) || defined(IRM_DIV_CHECK)
     if (set_device(c)) return IRM_EDEVICE;
     const int n = std::min(max_blocks, c->prof_blocks);
     if (n <= 0 || !c->d_prof) return 0;
@@ -1145,8 +1145,8 @@ int irm_optimize_batch_dev(irm_ctx* c, const irm_batch_dev* a, void* stream) {
     kp.trace = c->d_trace;
     kp.trace_cap = c->trace_cap;
     if (choose_shape(c, a->batch, true, kp, nullptr) <= 0) return fail(IRM_EINVAL, "no workgroup shape fits LDS");
-#ifdef IRM_PHASE_PROFILE
-    {
+#if defined(IRM_PHASE_PROFILE) || defined(IRM_DIV_CHECK)
+    {  // (IRM_DIV_CHECK: per-block counters of the BLS division check, zeroed per launch)
         const int grid = (a->batch + kp.TB - 1) / kp.TB;
         if (grid > c->prof_cap) {
             if (c->d_prof) (void)hipFree(c->d_prof);
@@ -1156,6 +1156,9 @@ int irm_optimize_batch_dev(irm_ctx* c, const irm_batch_dev* a, void* stream) {
         }
         c->prof_blocks = grid;
         kp.prof = c->d_prof;
+#ifdef IRM_DIV_CHECK
+        HIP_TRY(hipMemsetAsync(c->d_prof, 0, (size_t)grid * irm::kProfPhases * sizeof(unsigned long long), (hipStream_t)stream));
+#endif
     }
 #endif
     HIP_TRY(irm::launch_optimize(kp, (hipStream_t)stream));

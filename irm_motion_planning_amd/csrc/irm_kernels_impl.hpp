@@ -924,6 +924,25 @@ __device__ __forceinline__ float div_rcp(float a, float b, float r) {
     const float q = a * r;
     return fmaf(fmaf(-q, b, a), r, q);
 }
+// The IEEE quotient a/b in div_rcp's 3 VALU (round 6): with r = RN(1/b), the correctly rounded reciprocal
+// (shared by every quotient of the same divisor), q = RN(a·r) is within an ulp of a/b and the fma
+// correction RN(q + (a − q·b)·r) is the correctly rounded a/b (Markstein's theorem; normal operands, and a
+// remainder a − q·b above the subnormal range).  RN(1/b) itself: one Newton step from v_rcp_f32 (faithful,
+// ≤ 1 ulp) is the correctly rounded reciprocal for every divisor but those with an all-ones mantissa
+// (b = 2^e·(2 − 2^-23)), whose RN(1/b) = 2^(−e−1)·(1 + 2^-23) has the bit pattern 0x7F000000 − bits(b) (b > 0)
+// and is selected there (branch-free: a branch here split the trial stage's block, C3-BLS faithful +2 %).
+// tests/test_division.py checks both statements on the host (every divisor mantissa); the IRM_DIV_CHECK build
+// counts the kernel's mismatches against __fdiv_rn (tools/div_check.py → profiles/r06_div_check.txt: 0).
+// The BLS step direction ĝ = G/‖G‖ (optimizer_BLS.py:165) uses it (b = ‖G‖ > 0, normal).
+__device__ __forceinline__ float rcp_rn(float b) {
+    const float r = rcp_refined(b);
+#ifdef IRM_X_RCP_OLD
+    return r;
+#else
+    const unsigned u = __float_as_uint(b);
+    return (u & 0x7fffffu) == 0x7fffffu ? __uint_as_float(0x7F000000u - u) : r;
+#endif
+}
 
 // One f32x4 of an operator fragment array through a buffer descriptor: the per-lane part of the address in
 // one VGPR (voff, shared by every load of a stream), the wave-uniform part (tile, k-quad) in soff — a
@@ -2674,7 +2693,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #ifdef IRM_X_GLATE_ALL
     constexpr bool kGLate = !BLS && !DENSE && kS2Fix && kS2Batch;
 #else
-    constexpr bool kGLate = GD1 && D <= 3 && kS2Fix && kS2Batch;
+    // (WPTL > 1 only: glate_tiles' waves write G rows of trajectories they do not own, and with one wave per
+    // trajectory — N ≤ 64 — only a wave barrier would sit between that write and the owner's read)
+    constexpr bool kGLate = GD1 && D <= 3 && kS2Fix && kS2Batch && WPTL > 1;
 #endif
     f32x4 glY0 = f32x4{0.f, 0.f, 0.f, 0.f}, glY1 = f32x4{0.f, 0.f, 0.f, 0.f};
     // (kGLate) the G tiles, issued right after the stage-2 barrier: their MFMAs under the update /
@@ -3040,8 +3061,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         }
         const float lrx = (hmr && cl / D == hsr) ? lrs * P.bls_bm : lrs;  // a helper: t*'s next trial (:147)
         const float cjx = unfused(1.f - unfused(P.lreg * lrx));            // optimizer_BLS.py:139
-        // ĝ = G/‖G‖ (optimizer_BLS.py:165) and the step lr/‖G‖ through one refined reciprocal (div_rcp)
-        const float rg = rcp_refined(gn);
+        // ĝ = G/‖G‖ (optimizer_BLS.py:165) and the step lr/‖G‖: IEEE quotients through the correctly
+        // rounded reciprocal (div_rcp with rcp_rn)
+        const float rg = rcp_rn(gn);
         const float sx = div_rcp(lrx, gn, rg);  // the trajectory lanes' step (the same expression there)
         const float ne = -rcp_refined(fmaxf(sx, kMinRefStep));
         f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -3051,6 +3073,15 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 const float gh = div_rcp(G[i], gn, rg);
+#ifdef IRM_DIV_CHECK
+                if (act && pz < MTG) {  // diagnostics: ĝ against the IEEE division, and round 5's refined-rcp form
+                    const unsigned mis = __fdiv_rn(G[i], gn) != gh ? 1u : 0u;
+                    const unsigned mis5 = __fdiv_rn(G[i], gn) != div_rcp(G[i], gn, rcp_refined(gn)) ? 1u : 0u;
+                    atomicAdd(&P.prof[(size_t)blockIdx.x * kProfPhases + 0], (unsigned long long)mis);
+                    atomicAdd(&P.prof[(size_t)blockIdx.x * kProfPhases + 1], (unsigned long long)mis5);
+                    atomicAdd(&P.prof[(size_t)blockIdx.x * kProfPhases + 2], 1ull);
+                }
+#endif
                 // α_j = fl(fl(c·α) − fl(lr·ĝ)) (optimizer_BLS.py:139) and its scaled residual e' = (c·α − α_j)/s − G,
                 // u = fl(c·α − α_j) in one rounding (alpha_step_gd2's form: e' to 2^-24 of |G|)
                 const float p1 = unfused(cjx * A[i]), p2 = unfused(lrx * gh);
@@ -3421,6 +3452,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // the older one in every phase; static priority for that half (MI355X_MICROARCH.md, two waves per
     // SIMD, item 4): C3 +1.7 %.  Priority only reorders issue: results are unchanged.
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+    bool hm_prev = false;  // (kHelp) the previous round was a helper round: its priorities are still set
     for (int par = 0;; par ^= 1) {
         f32x4 pre1[KQU1], pre1w[KQU1];
         f32x4 zpre[kZPre ? kKQZ : 1];
@@ -3477,6 +3509,13 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 if (t == ts) __builtin_amdgcn_s_setprio(3);
                 else __builtin_amdgcn_s_setprio(0);
             }
+#ifndef IRM_X_NOPRIO_RESTORE
+            else if (hm_prev) {  // back to the launch's split (waves 4-7 at 1) once the helper rounds end
+                if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
+#endif
+            hm_prev = hm;
             // t* publishes its α, T, V for the helper at the top of each helper round (the helper reads them
             // after this round's G-tile barrier), instead of after every accepted trial of every trajectory
             if constexpr (kSSLazy) {
@@ -3588,7 +3627,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 gnj = h_gn;
             }
             cj = unfused(1.f - unfused(P.lreg * lrj));  // (1 − λ_reg·bls_lr) in fp32 (optimizer_BLS.py:139)
-            stepj = div_rcp(lrj, gnj, rcp_refined(gnj));  // bls_gz's step, bit for bit
+            stepj = div_rcp(lrj, gnj, rcp_rn(gnj));  // bls_gz's step, bit for bit
         }
         // ------------------------------------------------ end of an inner loop: α's exact trajectory
         if (rsy) {  // block-uniform

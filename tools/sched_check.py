@@ -29,18 +29,24 @@ CASES = [  # (name, config, faithful, batch, general kernel, optimizer override)
     ("c7_bls", "c7", True, 16, False, "bls"),
     ("c5_dense", "c5", False, 32, False, None, -1),  # (operator rank) k_optimize at R = N, L2 operands
     ("c3_dense_faithful", "c3", True, 32, False, None, -1),
+    # the GD single loop at one wave per trajectory (N ≤ 64: no G tiles after the stage-2 barrier there)
+    ("n50_bench_lean", "c3", False, 256, False, None, 0, {"n_timesteps": 50}),
+    ("n64_bench_lean", "c3", False, 256, False, None, 0, {"n_timesteps": 64}),
 ]
 
 
 def run(out):
     res = {}
     only = os.environ.get("IRM_CASES")
-    for name, cfg, faithful, B, general, opt, *rank in CASES:
+    for name, cfg, faithful, B, general, opt, *extra in CASES:
         if only and name not in only.split(","):
             continue
+        rank = [extra[0]] if extra and extra[0] else []
         args = bench.make_args(cfg, faithful, 200)
         if opt:
             args.optimizer_name = opt
+        for k, v in (extra[1] if len(extra) > 1 else {}).items():
+            setattr(args, k, v)
         s, g, obs = bench.make_problem(cfg, 1, 0)
         if general:
             os.environ["IRM_GENERAL_KERNEL"] = "1"
