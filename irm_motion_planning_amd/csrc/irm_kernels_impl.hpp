@@ -930,12 +930,11 @@ __device__ __forceinline__ float div_rcp(float a, float b, float r) {
 // remainder a − q·b above the subnormal range).  RN(1/b) itself: one Newton step from v_rcp_f32 (faithful,
 // ≤ 1 ulp) is the correctly rounded reciprocal for every divisor but those with an all-ones mantissa
 // (b = 2^e·(2 − 2^-23)), whose RN(1/b) = 2^(−e−1)·(1 + 2^-23) has the bit pattern 0x7F000000 − bits(b) (b > 0)
-// and is selected there (branch-free: a branch here split the trial stage's block, C3-BLS faithful +2 %).
+// and is selected there (branch-free; a branch here split the trial stage's block).
 // tests/test_division.py checks both statements on the host (every divisor mantissa); the IRM_DIV_CHECK build
 // counts the kernel's mismatches against __fdiv_rn (tools/div_check.py → profiles/r06_div_check.txt: 0).
 // The BLS step direction ĝ = G/‖G‖ (optimizer_BLS.py:165) uses it (b = ‖G‖ > 0, normal).
-__device__ __forceinline__ float rcp_rn(float b) {
-    const float r = rcp_refined(b);
+__device__ __forceinline__ float rcp_rn_of(float b, float r) {  // r = rcp_refined(b)
 #ifdef IRM_X_RCP_OLD
     return r;
 #else
@@ -3061,10 +3060,11 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
         }
         const float lrx = (hmr && cl / D == hsr) ? lrs * P.bls_bm : lrs;  // a helper: t*'s next trial (:147)
         const float cjx = unfused(1.f - unfused(P.lreg * lrx));            // optimizer_BLS.py:139
-        // ĝ = G/‖G‖ (optimizer_BLS.py:165) and the step lr/‖G‖: IEEE quotients through the correctly
-        // rounded reciprocal (div_rcp with rcp_rn)
-        const float rg = rcp_rn(gn);
-        const float sx = div_rcp(lrx, gn, rg);  // the trajectory lanes' step (the same expression there)
+        // ĝ = G/‖G‖ (optimizer_BLS.py:165): the IEEE quotient through the correctly rounded reciprocal (div_rcp
+        // with rcp_rn_of); the waypoint-space step s = lr/‖G‖ (not reference arithmetic: the residual e'
+        // absorbs its rounding) through the refined one, as the trajectory lanes form it
+        const float rr = rcp_refined(gn), rg = rcp_rn_of(gn, rr);
+        const float sx = div_rcp(lrx, gn, rr);  // the trajectory lanes' step (the same expression there)
         const float ne = -rcp_refined(fmaxf(sx, kMinRefStep));
         f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
         auto tile = [&](int u, f32x4 G, bool store_g, f32x4 A, f32x4 a) {  // α rows, V_Rᵀ fragment (rank tile 0)
@@ -3452,7 +3452,9 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
     // the older one in every phase; static priority for that half (MI355X_MICROARCH.md, two waves per
     // SIMD, item 4): C3 +1.7 %.  Priority only reorders issue: results are unchanged.
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#ifdef IRM_X_PRIO_RESTORE
     bool hm_prev = false;  // (kHelp) the previous round was a helper round: its priorities are still set
+#endif
     for (int par = 0;; par ^= 1) {
         f32x4 pre1[KQU1], pre1w[KQU1];
         f32x4 zpre[kZPre ? kKQZ : 1];
@@ -3509,13 +3511,16 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 if (t == ts) __builtin_amdgcn_s_setprio(3);
                 else __builtin_amdgcn_s_setprio(0);
             }
-#ifndef IRM_X_NOPRIO_RESTORE
-            else if (hm_prev) {  // back to the launch's split (waves 4-7 at 1) once the helper rounds end
+            // (the helper priorities stay set in the rounds after a helper round — a lone trajectory's resync
+            // rounds: t* keeps the issue lead there.  Restoring the launch's split once the helper rounds end,
+            // IRM_X_PRIO_RESTORE, measured C3-BLS faithful +0.8 %, C2 even; priority only reorders issue)
+#ifdef IRM_X_PRIO_RESTORE
+            else if (hm_prev) {  // back to the launch's split (waves 4-7 at 1)
                 if (wave >= 4) __builtin_amdgcn_s_setprio(1);
                 else __builtin_amdgcn_s_setprio(0);
             }
-#endif
             hm_prev = hm;
+#endif
             // t* publishes its α, T, V for the helper at the top of each helper round (the helper reads them
             // after this round's G-tile barrier), instead of after every accepted trial of every trajectory
             if constexpr (kSSLazy) {
@@ -3627,7 +3632,7 @@ __global__ __launch_bounds__(MAXT, (MAXT <= 256 && WPL == 1) ? 2 : 1) void k_lea
                 gnj = h_gn;
             }
             cj = unfused(1.f - unfused(P.lreg * lrj));  // (1 − λ_reg·bls_lr) in fp32 (optimizer_BLS.py:139)
-            stepj = div_rcp(lrj, gnj, rcp_rn(gnj));  // bls_gz's step, bit for bit
+            stepj = div_rcp(lrj, gnj, rcp_refined(gnj));  // bls_gz's step, bit for bit
         }
         // ------------------------------------------------ end of an inner loop: α's exact trajectory
         if (rsy) {  // block-uniform

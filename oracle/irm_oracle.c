@@ -687,6 +687,8 @@ static void optimize_gd(const orc_ctx* c, float* alpha, const float* obs, int O,
 typedef struct {
     float* buf;
     int32_t cap, n;
+    int32_t snap_row; /* orc_trial_iterate: the trial iterate of log row snap_row goes to snap */
+    float* snap;
 } bls_trace;
 
 static void trace_put(bls_trace* tr, int outer, int inner, int trial, float lr, float nl, float req, int acc,
@@ -738,6 +740,7 @@ static void optimize_bls(const orc_ctx* c, float* alpha, const float* obs, int O
                 st->cost_evals++;
                 st->bls_trials++;
                 float required = loss - p->bls_alpha * lr * anorm;
+                if (trc && trc->snap && trc->n == trc->snap_row) memcpy(trc->snap, na, sizeof(float) * ND);
                 trace_put(trc, outer, it, j, lr, nl, required, !(nl > required), loss, nrm, anorm);
                 if (nl > required) {
                     lr = lr * p->bls_beta_minus;
@@ -781,7 +784,7 @@ int32_t orc_optimize_trace(const orc_ctx* c, const float* alpha0, const float* o
                            float* trace, int32_t trace_cap) {
     irm_stats st;
     memset(&st, 0, sizeof(st));
-    bls_trace tr = {trace, trace_cap, 0};
+    bls_trace tr = {trace, trace_cap, 0, -1, NULL};
     memcpy(alpha_out, alpha0, sizeof(float) * c->N * c->D);
     snapshot(c, alpha_out, series, max_series, &st.series_len); /* row 0 = initial trajectory */
     if (c->p.optimizer == IRM_OPT_BLS)
@@ -790,6 +793,22 @@ int32_t orc_optimize_trace(const orc_ctx* c, const float* alpha0, const float* o
         optimize_gd(c, alpha_out, obstacles, O, s, g, &st, series, max_series);
     if (stats) *stats = st;
     return tr.n;
+}
+
+/* Test diagnostics: the fp32 trial iterate α_j = (1 − λ_reg·lr)·α − lr·ĝ of line-search log row `row`
+   (optimizer_BLS.py:139) of a BLS run from alpha0 — e.g. to find the loss's penalty-mask thresholds
+   (trajectory.py:221-222, 251) near a trial whose accept / reject two runs decide differently.
+   Returns 1 if the run reached that row. */
+int32_t orc_trial_iterate(const orc_ctx* c, const float* alpha0, const float* obstacles, int32_t O, const float* s,
+                          const float* g, int32_t row, float* out) {
+    irm_stats st;
+    memset(&st, 0, sizeof(st));
+    float a[IRM_MAX_TIMESTEPS * IRM_MAX_JOINTS];
+    bls_trace tr = {NULL, 0, 0, row, out};
+    memcpy(a, alpha0, sizeof(float) * c->N * c->D);
+    if (c->p.optimizer != IRM_OPT_BLS) return 0;
+    optimize_bls(c, a, obstacles, O, s, g, &st, NULL, 0, &tr);
+    return tr.n > row ? 1 : 0;
 }
 
 void orc_optimize(const orc_ctx* c, const float* alpha0, const float* obstacles, int32_t O, const float* s,

@@ -50,6 +50,8 @@ void orc_optimize(const orc_ctx* c, const float* alpha0, const float* obstacles,
  * new_loss, required_loss, accepted, loss, ‖g‖, alpha_norm), at most trace_cap records; returns the
  * number of trials (may exceed trace_cap). */
 #define ORC_TRACE_W 10
+int32_t orc_trial_iterate(const orc_ctx* c, const float* alpha0, const float* obstacles, int32_t O, const float* s,
+                          const float* g, int32_t row, float* out);
 int32_t orc_optimize_trace(const orc_ctx* c, const float* alpha0, const float* obstacles, int32_t O, const float* s,
                            const float* g, float* alpha_out, irm_stats* stats, float* series, int32_t max_series,
                            float* trace, int32_t trace_cap);

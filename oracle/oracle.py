@@ -53,6 +53,8 @@ def _load():
         lib.orc_optimize_trace.restype = ctypes.c_int32
         lib.orc_optimize_trace.argtypes = [ctypes.c_void_p, _fp, _fp, ctypes.c_int32, _fp, _fp, _fp,
                                            ctypes.POINTER(IrmStats), _fp, ctypes.c_int32, _fp, ctypes.c_int32]
+        lib.orc_trial_iterate.restype = ctypes.c_int32
+        lib.orc_trial_iterate.argtypes = [ctypes.c_void_p, _fp, _fp, ctypes.c_int32, _fp, _fp, ctypes.c_int32, _fp]
         lib.orc_optimize.argtypes = [ctypes.c_void_p, _fp, _fp, ctypes.c_int32, _fp, _fp, _fp,
                                      ctypes.POINTER(IrmStats), _fp, ctypes.c_int32]
         lib.orc_optimize_batch.argtypes = [ctypes.c_void_p, _fp, _fp, _fp, _fp, ctypes.c_int32, ctypes.c_int32,
@@ -175,6 +177,15 @@ class Oracle:
         n = _load().orc_optimize_trace(self._c, _p(_f(alpha0)), _p(obs), obs.shape[0], _p(_f(s)), _p(_f(g)), _p(out),
                                    ctypes.byref(st), None, 0, _p(tr), cap)
         return out, stats_dict(st), tr[:min(n, cap)]
+
+    def trial_iterate(self, alpha0, obstacles, s, g, row):
+        """The BLS trial iterate α_j of line-search log row `row` of optimize_trace from alpha0 (None if the
+        run has fewer rows)."""
+        obs = _f(obstacles)
+        out = np.zeros((self.N, self.D), np.float32)
+        ok = _load().orc_trial_iterate(self._c, _p(_f(alpha0)), _p(obs), obs.shape[0], _p(_f(s)), _p(_f(g)), int(row),
+                                       _p(out))
+        return out if ok else None
 
     def optimize_batch(self, alpha0, start, goal, obstacles, obstacle_stride=0, n_threads=0):
         start = _f(start)

@@ -1,7 +1,7 @@
-"""The BLS step direction's quotient (irm_kernels_impl.hpp, div_rcp with rcp_rn): with r = RN(1/b),
+"""The BLS step direction's quotient (irm_kernels_impl.hpp, div_rcp with rcp_rn_of): with r = RN(1/b),
 q = RN(a·r) and RN(q + (a − q·b)·r) must be the IEEE quotient RN(a/b) — optimizer_BLS.py:165's
 ĝ = g / norm.  And r itself: one Newton step RN(y + y·RN(1 − b·y)) from either faithful rounding y of 1/b
-(v_rcp_f32 is faithful) must give RN(1/b) for every divisor mantissa but all-ones, where rcp_rn selects
+(v_rcp_f32 is faithful) must give RN(1/b) for every divisor mantissa but all-ones, where rcp_rn_of selects
 RN(1/b) by its bit pattern 0x7F000000 − bits(b).  Checked on the host in C (fmaf, -ffp-contract=off) for every divisor mantissa
 (2^23 values) against 16 dividends each, and for 2^26 random pairs over exponents far beyond
 what the kernel sees (‖G‖ from 2^-40 to 2^40, |ĝ| = |G|/‖G‖ from 2^-60 to 4 — |ĝ| ≤ 1 up to ‖G‖'s

@@ -1241,6 +1241,22 @@ def loss_drift(tr, ref, k):
     return float(max(np.max(np.abs(tr[:k, 7] - ref[:k, 7]) / den), np.max(np.abs(tr[:k, 5] - ref[:k, 5]) / den)))
 
 
+def mask_margin(o, a0, obs, s, g, row, p):
+    """Relative distance of the oracle's trial iterate at line-search log row `row` (trajectory and
+    velocities) from the penalty masks' thresholds (trajectory.py:221-222, 251: 0.98 × the joint limits,
+    --constraint-violating-dependant-loss): the masked penalty jumps there, so a trial whose point sits on
+    a threshold has a discontinuous loss and two runs may decide it differently whatever the Armijo margin."""
+    aj = o.trial_iterate(a0, obs, s, g, row)
+    if aj is None or not p.constraint_violating_dependant_loss:
+        return np.inf
+    T, V = o.evaluate(aj, 0), o.evaluate(aj, 1)
+    hi = p.joint_safety_limit * p.max_joint_position
+    lo = p.joint_safety_limit * p.min_joint_position
+    vt = p.joint_safety_limit * p.max_joint_velocity
+    return float(min(np.min(np.abs(T - hi)) / abs(hi), np.min(np.abs(T - lo)) / abs(lo),
+                     np.min(np.abs(np.abs(V) - vt)) / vt))
+
+
 def test_batched_bls_end_state_inside_oracle_ensemble():
     """The BLS dual loop (optimizer_BLS.py:127-213, the reference's default) end to end at four
     trajectories per workgroup, on all 64 problems of the batch.  BLS is chaotic (a 1e-7
@@ -1248,10 +1264,16 @@ def test_batched_bls_end_state_inside_oracle_ensemble():
     quality criterion (conftest.check_quality) against the oracle's ensemble from α0 and α0 ± 1 ulp (four
     draws): average / maximum obstacle cost no worse than the ensemble's worst + 0.01 and no better than
     its best − 0.03, a constraint flag the ensemble produced.  A problem outside that band (or with a flag
-    the ensemble did not produce) must have left the oracle's path at a knife edge: its line-search log (moved to batch index 0) follows the oracle's
-    decision for decision up to a decision whose relative margin is at most min(BLS_KNIFE_FACTOR × the
-    loss drift up to it, BLS_KNIFE_CAP) (floor BLS_KNIFE_FLOOR), the drift at most BLS_DRIFT_CAP; at most
-    BLS_KNIFE_MAX of the 64 problems may take that exit."""
+    the ensemble did not produce) must have left the oracle's path at a knife edge: its line-search log
+    (moved to batch index 0) follows the oracle's decision for decision up to a decision that two runs
+    this close may take differently — knife = max(min(BLS_KNIFE_FACTOR × the loss drift up to it,
+    BLS_KNIFE_CAP), BLS_KNIFE_FLOOR), the drift at most BLS_DRIFT_CAP — either
+      * an Armijo / loop_loss_reduction margin ≤ knife (optimizer_BLS.py:172-178), or
+      * a trial whose point lies within knife (relative) of a penalty-mask threshold (mask_margin): the
+        masked penalty is discontinuous there (measured in round 6: problem 60's first flip has an Armijo
+        margin of 1.7e-3, but its trial has a joint velocity 3.2e-5 from 0.98·v_max, where the penalty
+        jumps by λjl·½·0.98²/N = 3.8e-2 — the two runs' trial losses part by 1.3 %);
+    at most BLS_KNIFE_MAX of the 64 problems may take that exit."""
     import bench
     from conftest import BETTER_TOL, QUALITY_TOL
     from oracle.oracle import Oracle
@@ -1296,10 +1318,18 @@ def test_batched_bls_end_state_inside_oracle_ensemble():
               f"(oracle [{e[:, 1].min():.4f}, {e[:, 1].max():.4f}]) ok {ok} (oracle {sorted(oks)}) outside the "
               f"ensemble's band: first decision flip {flip}, loss drift before it {drift:.2e}")
         assert flip is not None and drift <= BLS_DRIFT_CAP, (b, flip, drift)
-        assert flip[1] <= max(min(BLS_KNIFE_FACTOR * drift, BLS_KNIFE_CAP), BLS_KNIFE_FLOOR), (b, flip, drift)
-        knife.append((b, flip[1], drift))
+        knife_m = max(min(BLS_KNIFE_FACTOR * drift, BLS_KNIFE_CAP), BLS_KNIFE_FLOOR)
+        kind, margin = "decision", float(flip[1])
+        if margin > knife_m:  # the flipped trial on a penalty-mask threshold (the trial row, or its predecessor
+            k = flip[0]       # for a loop_loss_reduction flip)
+            mm = min(mask_margin(o, a0[b], obs, s[b], g[b], r, args) for r in (k, k - 1) if r >= 0)
+            kind, margin = "mask", mm
+            print(f"  Armijo margin {float(flip[1]):.1e} above the knife edge {knife_m:.1e}: the trial's distance to a "
+                  f"penalty-mask threshold {mm:.1e}")
+        assert margin <= knife_m, (b, flip, drift, kind, margin)
+        knife.append((b, kind, margin, drift))
     print(f"{B} problems: {B - len(knife)} inside the oracle ensemble's band, {len(knife)} through a knife edge "
-          f"(margins {[f'{m:.1e}' for _, m, _ in knife]})")
+          f"({[f'{b}: {k} {m:.1e} (drift {d:.1e})' for b, k, m, d in knife]})")
     assert len(knife) <= BLS_KNIFE_MAX, knife
 
 

@@ -284,3 +284,22 @@ def test_oracle_outer_iteration_edge_cases():
     a, st = ob.optimize(a0, obstacles(), START, GOAL)
     np.testing.assert_array_equal(a, a0)
     assert st["grad_evals"] == 0 and st["outer_iterations"] == 0
+
+
+def test_oracle_trial_iterate_reproduces_the_log():
+    """orc_trial_iterate (the diagnostics of the BLS end-state test's mask knife edge) returns the trial
+    iterate of a log row: its loss is that row's new_loss (optimizer_BLS.py:139-140), bit for bit."""
+    from oracle.oracle import Oracle
+    from irm_motion_planning_amd.main import parse_args
+    from irm_motion_planning_amd.params import params_from_args
+    from irm_motion_planning_amd.environment import GOAL_CONFIG, OBSTACLES, START_CONFIG
+    args = parse_args(["--max-outer-iteration", "2"])
+    o = Oracle(params_from_args(args))
+    a0 = o.init_alpha(START_CONFIG, GOAL_CONFIG)
+    _, _, tr = o.optimize_trace(a0, OBSTACLES, START_CONFIG, GOAL_CONFIG, cap=4096)
+    for row in (0, 1, len(tr) // 2, len(tr) - 1):
+        aj = o.trial_iterate(a0, OBSTACLES, START_CONFIG, GOAL_CONFIG, row)
+        lsg = args.lambda_sg_constraint * args.lambda_constraint_increase ** int(tr[row, 0])
+        ljl = args.lambda_jl_constraint * args.lambda_constraint_increase ** int(tr[row, 0])
+        assert np.float32(o.cost(aj, OBSTACLES, START_CONFIG, GOAL_CONFIG, lsg, ljl, args.lambda_max_cost)) == tr[row, 4]
+    assert o.trial_iterate(a0, OBSTACLES, START_CONFIG, GOAL_CONFIG, len(tr)) is None

@@ -46,6 +46,8 @@ for nohelp in ("0", "1"):
     drift = loss_drift(strip, tro, flip[0]) if flip else 0.0
     print(f"helpers {'off' if nohelp == '1' else 'on'}: {len(tr)} trials, grad evals {int(st['grad_evals'][0])}, "
           f"ok {int(st['constraints_ok'][0])}, first flip {flip}, drift {drift:.2e}")
+    if nohelp == "0":
+        np.savez(os.path.join("gpurun_out", f"flip{P}.npz"), a0=a0, tr=tr, tro=tro)
     if flip:
         k = flip[0]
         cols = "outer inner trial lr new_loss required acc loss |g| anorm"
@@ -53,3 +55,30 @@ for nohelp in ("0", "1"):
         print(tr[max(0, k - 4):k + 3])
         print("   oracle rows")
         print(tro[max(0, k - 4):k + 3])
+
+# The max-cost argmax (trajectory.py:97) along both runs: the extended-vis frames (one per accepted inner
+# iteration; the kernel's own waypoint state) of the kernel and the oracle from the same α0 — the first
+# frame whose max-cost waypoints differ, and the two runs' relative potential gaps between them there.
+from oracle.oracle import compute_cost_vg  # noqa: E402
+os.environ["IRM_LEAN_NOHELP"] = "0"
+os.environ.pop("IRM_TRACE_PROBLEM", None)
+c = Context(params_from_args(args, traj_per_block=4))
+_, _, st, ser = c.optimize(s[idx], g[idx], obs, series=True)
+fk = ser[0][: int(st["series_len"][0])]
+_, so, fo = o.optimize(a0, obs, s[P], g[P], max_series=4096)
+n = min(len(fk), len(fo))
+print(f"frames: kernel {len(fk)}, oracle {len(fo)}; |traj| diff at frames 0, 1, 2, 5, 10, 20, 30:",
+      [f"{np.abs(fk[i] - fo[i]).max():.1e}" for i in (0, 1, 2, 5, 10, 20, 30) if i < n])
+drift = 0.0
+for i in range(n):
+    cg = compute_cost_vg(o.fk(fk[i]), obs)[0]
+    co = compute_cost_vg(o.fk(fo[i]), obs)[0]
+    ag, ao = int(np.argmax(cg)), int(np.argmax(co))
+    if ag != ao:
+        m = min((cg[ag] - cg[ao]) / cg[ag], (co[ao] - co[ag]) / co[ao])
+        print(f"frame {i}: max-cost waypoint kernel {ag} / oracle {ao}, margin {m:.2e}, potential drift before {drift:.2e}, "
+              f"|traj| diff {np.abs(fk[i] - fo[i]).max():.2e}")
+        break
+    drift = max(drift, float(np.max(np.abs(cg - co)) / np.max(co)))
+else:
+    print(f"{n} frames: the same max-cost waypoint throughout")

@@ -4,7 +4,7 @@
     IRM_LIB=…/libirm_hip_divchk.so python tools/div_check.py  (GPU box)
 
 The IRM_DIV_CHECK build compares, for every element of every line-search trial the fused trial stages
-form (bls_gz, irm_kernels_impl.hpp), the shipped quotient div_rcp(G, ‖G‖, rcp_rn(‖G‖)) and round 5's
+form (bls_gz, irm_kernels_impl.hpp), the shipped quotient div_rcp(G, ‖G‖, rcp_rn_of(‖G‖, ·)) and round 5's
 div_rcp(G, ‖G‖, rcp_refined(‖G‖)) against __fdiv_rn(G, ‖G‖), and counts per workgroup.  Runs the
 reference's default flow (BLS, faithful) on all 1024 C3 problems and on C2."""
 import ctypes
