@@ -205,11 +205,13 @@ def cpu_budgets(world):
 
 
 def rendezvous_timeout(world):
-    """init_process_group's timeout: rank 0's capped CPU-baseline work (measured sample ≈ budget, plus the
-    1-thread calibration runs and the worker pool's start-up) with a wide margin — bounded, not the
-    backend's default."""
+    """init_process_group's timeout: it bounds the rendezvous, where the other ranks wait for rank 0's
+    capped CPU-baseline work (measured sample ≈ budget, plus the 1-thread calibration runs and the worker
+    pool's start-up: ≤ 120 + 10 × the budgets with a wide margin), and it also becomes the timeout of every
+    later collective (the barriers around the warm-up and the timed loop), so it is never below the RCCL
+    default of 10 minutes: a slow rank in context set-up or warm-up does not trip the watchdog early."""
     import datetime
-    return datetime.timedelta(seconds=int(120 + 10 * sum(cpu_budgets(world))))
+    return datetime.timedelta(seconds=max(600, int(120 + 10 * sum(cpu_budgets(world)))))
 
 
 def cpu_baseline(cfg, args, start, goal, obstacles, world=1):

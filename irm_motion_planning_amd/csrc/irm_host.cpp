@@ -722,7 +722,10 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
         kp.thr_v = (float)((double)p->joint_safety_limit * (double)p->max_joint_velocity);
         // --constraint-violating-dependant-loss false (trajectory.py:221-222, 251: the penalties apply to
         // every element): thresholds that every finite joint position / velocity passes, so the kernels
-        // form the masks without the flag (one scalar op fewer per mask element and round)
+        // form the masks without the flag (one scalar op fewer per mask element and round).  Deliberate
+        // deviation: a NaN joint value fails every compare, so its penalty term is masked
+        // off (0) where the reference's unmasked penalty would carry the NaN into the loss — only a diverged
+        // trajectory (non-finite state) can see the difference, and its loss is non-finite either way
         if (!p->constraint_violating_dependant_loss) {
             kp.thr_hi = -INFINITY;
             kp.thr_lo = INFINITY;
