@@ -1369,3 +1369,41 @@ def test_general_kernel_bls_follows_oracle_trial_for_trial(case, argv, ov):
     np.testing.assert_allclose(a[:, 7], r[:, 7], rtol=1e-5)  # loss at α
     np.testing.assert_allclose(a[:, 8], r[:, 8], rtol=1e-4)  # ‖g‖
     np.testing.assert_allclose(a[:, 9], r[:, 9], rtol=1e-4)  # alpha_norm
+
+
+def test_bls_step_direction_is_the_ieee_quotient():
+    """ĝ = G/‖G‖ (optimizer_BLS.py:165) in the BLS trial stages is the IEEE quotient: the IRM_DIV_CHECK build
+    of the same sources (python -m irm_motion_planning_amd.build --divchk) compares every ĝ element the
+    trial stages form with __fdiv_rn and counts the mismatches per workgroup (irm_debug_phase_profile's
+    buffer); C2 and 64 C3-BLS problems in the reference's flow: none (the full C3-BLS batch:
+    tools/div_check.py → profiles/r06_div_check.txt).  Skipped without that build, or if it was built from
+    other sources."""
+    import ctypes
+    import bench
+    from irm_motion_planning_amd import build
+    from irm_motion_planning_amd._abi import load_library
+    from irm_motion_planning_amd.context import Context
+    from irm_motion_planning_amd.params import params_from_args
+    path = os.path.join(os.path.dirname(build.OUT), build.VARIANTS["divchk"][0])
+    if not os.path.exists(path):
+        pytest.skip("no IRM_DIV_CHECK library (python -m irm_motion_planning_amd.build --divchk)")
+    lib = load_library(path)
+    if lib.irm_build_id().decode() != build.source_hash("divchk"):
+        pytest.skip("the IRM_DIV_CHECK library was built from other sources")
+    for cfg, B in (("c2", 1), ("c3bls", 64)):
+        p = params_from_args(bench.make_args(cfg, True, 200))
+        c = Context.__new__(Context)  # a context of the division-check library
+        c.lib, c.params, c.N, c.D = lib, p, int(p.n_timesteps), int(p.n_joints)
+        h = ctypes.c_void_p()
+        assert lib.irm_ctx_create(ctypes.byref(h), ctypes.byref(p)) == 0
+        c._h = h
+        s, g, obs = bench.make_problem(cfg, 1, 0)
+        _, _, st = c.optimize(s[:B], g[:B], obs)
+        K = 24
+        buf = (ctypes.c_uint64 * (256 * K))()
+        n = lib.irm_debug_phase_profile(h, buf, 256)
+        cnt = np.frombuffer(buf, dtype=np.uint64, count=n * K).reshape(n, K)
+        mis, tot = int(cnt[:, 0].sum()), int(cnt[:, 2].sum())
+        print(f"{cfg}: {int(np.sum(st['bls_trials']))} line-search trials, {tot} quotients, {mis} differ from the IEEE division")
+        assert tot > 1000 * B and mis == 0
+        c.close()
