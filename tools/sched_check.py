@@ -32,6 +32,12 @@ CASES = [  # (name, config, faithful, batch, general kernel, optimizer override)
     # the GD single loop at one wave per trajectory (N ≤ 64: no G tiles after the stage-2 barrier there)
     ("n50_bench_lean", "c3", False, 256, False, None, 0, {"n_timesteps": 50}),
     ("n64_bench_lean", "c3", False, 256, False, None, 0, {"n_timesteps": 64}),
+    # the BLS flow: its bench mode (every trial round of 200 inner iterations, all-rejected searches going on
+    # at the same α), the reference flow on a whole batch, and the one-wave-per-trajectory shapes
+    ("c3bls_bench", "c3bls", False, 256, False, None),
+    ("c3bls_faithful", "c3bls", True, 256, False, None),
+    ("n64_bls", "c3", True, 64, False, "bls", 0, {"n_timesteps": 64}),
+    ("n50_bls", "c3", True, 64, False, "bls", 0, {"n_timesteps": 50}),
 ]
 
 
@@ -58,6 +64,7 @@ def run(out):
         res[name + "_traj"] = traj
         res[name + "_alpha"] = alpha
         res[name + "_evals"] = np.asarray(st["grad_evals"])
+        res[name + "_trials"] = np.asarray(st["bls_trials"])
         print(name, "done", flush=True)
     np.savez(out, **res)
 
