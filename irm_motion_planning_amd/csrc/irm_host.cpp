@@ -15,6 +15,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -58,43 +59,87 @@ int fail(int code, const char* fmt, ...) {
 // ------------------------------------------------------------- host linalg
 // Cyclic Jacobi eigen-decomposition of a symmetric n×n matrix (fp64).
 // On return a's diagonal holds the eigenvalues and v the eigenvectors (columns).
-void jacobi_eigen(std::vector<double>& a, int n, std::vector<double>& v) {
-    v.assign((size_t)n * n, 0.0);
-    for (int i = 0; i < n; ++i) v[(size_t)i * n + i] = 1.0;
+// The rotations work on copies with a padded row stride (a power-of-two stride put every element of a
+// column rotation into one cache set) and accumulate the eigenvectors as rows (vᵀ: each rotation updates
+// two contiguous rows): the same operations in the same order as the plain n-stride form, so the result
+// is bit-identical, 4.6× faster at n = 512 (108 → 23 s on one core; the context of an N = 512 trajectory).
+void jacobi_eigen(std::vector<double>& a_io, int n, std::vector<double>& v_out) {
+    const int ld = n + 8;
+    std::vector<double> a((size_t)n * ld), vt((size_t)n * ld, 0.0);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) a[(size_t)i * ld + j] = a_io[(size_t)i * n + j];
+    for (int i = 0; i < n; ++i) vt[(size_t)i * ld + i] = 1.0;
     double fro = 0.0;
-    for (double x : a) fro += x * x;
+    for (double x : a_io) fro += x * x;
     fro = sqrt(fro);
     for (int sweep = 0; sweep < 64; ++sweep) {
         double off = 0.0;
         for (int p = 0; p < n; ++p)
-            for (int q = p + 1; q < n; ++q) off += a[(size_t)p * n + q] * a[(size_t)p * n + q];
+            for (int q = p + 1; q < n; ++q) off += a[(size_t)p * ld + q] * a[(size_t)p * ld + q];
         if (sqrt(off) <= 1e-17 * fro) break;
         for (int p = 0; p < n; ++p) {
             for (int q = p + 1; q < n; ++q) {
-                double apq = a[(size_t)p * n + q];
+                double apq = a[(size_t)p * ld + q];
                 if (fabs(apq) <= 1e-300) continue;
-                double app = a[(size_t)p * n + p], aqq = a[(size_t)q * n + q];
+                double app = a[(size_t)p * ld + p], aqq = a[(size_t)q * ld + q];
                 double theta = (aqq - app) / (2.0 * apq);
                 double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
                 double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
                 for (int k = 0; k < n; ++k) {  // rotate columns p, q
-                    double akp = a[(size_t)k * n + p], akq = a[(size_t)k * n + q];
-                    a[(size_t)k * n + p] = c * akp - s * akq;
-                    a[(size_t)k * n + q] = s * akp + c * akq;
+                    double akp = a[(size_t)k * ld + p], akq = a[(size_t)k * ld + q];
+                    a[(size_t)k * ld + p] = c * akp - s * akq;
+                    a[(size_t)k * ld + q] = s * akp + c * akq;
                 }
+                double* ap = &a[(size_t)p * ld];
+                double* aq = &a[(size_t)q * ld];
                 for (int k = 0; k < n; ++k) {  // rotate rows p, q
-                    double apk = a[(size_t)p * n + k], aqk = a[(size_t)q * n + k];
-                    a[(size_t)p * n + k] = c * apk - s * aqk;
-                    a[(size_t)q * n + k] = s * apk + c * aqk;
+                    double apk = ap[k], aqk = aq[k];
+                    ap[k] = c * apk - s * aqk;
+                    aq[k] = s * apk + c * aqk;
                 }
-                for (int k = 0; k < n; ++k) {
-                    double vkp = v[(size_t)k * n + p], vkq = v[(size_t)k * n + q];
-                    v[(size_t)k * n + p] = c * vkp - s * vkq;
-                    v[(size_t)k * n + q] = s * vkp + c * vkq;
+                double* vp = &vt[(size_t)p * ld];
+                double* vq = &vt[(size_t)q * ld];
+                for (int k = 0; k < n; ++k) {  // eigenvector columns p, q (rows of vᵀ)
+                    double vkp = vp[k], vkq = vq[k];
+                    vp[k] = c * vkp - s * vkq;
+                    vq[k] = s * vkp + c * vkq;
                 }
             }
         }
     }
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) a_io[(size_t)i * n + j] = a[(size_t)i * ld + j];
+    v_out.assign((size_t)n * n, 0.0);
+    for (int i = 0; i < n; ++i)
+        for (int j = 0; j < n; ++j) v_out[(size_t)i * n + j] = vt[(size_t)j * ld + i];
+}
+
+// Eigen-decompositions of the operator Gram matrices already computed in this process, keyed by the
+// matrix itself (a context of the same N, σ and time grid reuses it: N = 512 takes ≈ 20 s to factorise).
+struct EigenMemo {
+    int n;
+    std::vector<double> g, a, v;  // input, decomposed a (eigenvalues on the diagonal), eigenvectors
+};
+std::mutex g_eigen_mu;
+std::vector<EigenMemo> g_eigen_memo;
+
+void jacobi_eigen_memo(std::vector<double>& a, int n, std::vector<double>& v) {
+    {
+        std::lock_guard<std::mutex> lk(g_eigen_mu);
+        for (const EigenMemo& m : g_eigen_memo)
+            if (m.n == n && m.g == a) {
+                a = m.a;
+                v = m.v;
+                return;
+            }
+    }
+    EigenMemo m{n, a, {}, {}};
+    jacobi_eigen(a, n, v);
+    m.a = a;
+    m.v = v;
+    std::lock_guard<std::mutex> lk(g_eigen_mu);
+    if (g_eigen_memo.size() >= 8) g_eigen_memo.erase(g_eigen_memo.begin());
+    g_eigen_memo.push_back(std::move(m));
 }
 
 /* fp32 LU with partial pivoting in LAPACK's recursive order (sgetrf2: factor the left half of the
@@ -505,14 +550,18 @@ int irm_ctx_create(irm_ctx** out, const irm_params* p) {
         for (int i = 0; i < N; ++i) Vd[(size_t)i * RP + i] = 1.0;
         c->trunc = 0.f;
     } else {
-        std::vector<double> G((size_t)N * N, 0.0), Vfull;
+        std::vector<double> G((size_t)N * N, 0.0), Vfull, LdT((size_t)N * 2 * N);
+        for (int m = 0; m < 2 * N; ++m)  // Lᵀ rows: the Gram sums read contiguously (same sums, same order)
+            for (int i = 0; i < N; ++i) LdT[(size_t)i * 2 * N + m] = Ld[(size_t)m * N + i];
         for (int i = 0; i < N; ++i)
             for (int j = i; j < N; ++j) {
                 double s = 0.0;
-                for (int m = 0; m < 2 * N; ++m) s += Ld[(size_t)m * N + i] * Ld[(size_t)m * N + j];
+                const double* li = &LdT[(size_t)i * 2 * N];
+                const double* lj = &LdT[(size_t)j * 2 * N];
+                for (int m = 0; m < 2 * N; ++m) s += li[m] * lj[m];
                 G[(size_t)i * N + j] = G[(size_t)j * N + i] = s;
             }
-        jacobi_eigen(G, N, Vfull);
+        jacobi_eigen_memo(G, N, Vfull);
         std::vector<int> order(N);
         for (int i = 0; i < N; ++i) order[i] = i;
         std::sort(order.begin(), order.end(),

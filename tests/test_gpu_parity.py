@@ -717,6 +717,53 @@ def test_large_batch_matches_small_batch():
     np.testing.assert_array_equal(t_big[3072:], t_small)
 
 
+@pytest.mark.parametrize("opt", ["gd", "bls"])
+def test_empty_batch(opt):
+    """B = 0: every batched entry point returns empty outputs and IRM_OK, without a launch (irm_host.cpp:
+    the `B == 0` early returns) — the reference has no batch, so an empty one must simply be a no-op."""
+    c = ctx("--optimizer-name", opt, "--max-inner-iteration", 5)
+    z3 = np.zeros((0, 3), np.float32)
+    za = np.zeros((0, 50, 3), np.float32)
+    obs = obstacles()
+    assert c.init_alpha(z3, z3).shape == (0, 50, 3)
+    assert c.evaluate(za).shape == (0, 50, 3)
+    assert np.asarray(c.eval_cost(za, obs, z3, z3, 0.5, 0.1, 0.5)).shape == (0,)
+    assert np.asarray(c.eval_cost_grad(za, obs, z3, z3, 0.5, 0.1, 0.5)).shape == (0, 50, 3)
+    alpha, traj, st = c.optimize(z3, z3, obs)
+    assert alpha.shape == (0, 50, 3) and traj.shape == (0, 50, 3) and len(st["grad_evals"]) == 0
+    # and the context still serves a real batch afterwards
+    _, traj1, st1 = c.optimize(np.zeros((1, 3), np.float32), np.full((1, 3), 0.5, np.float32), obs)
+    assert np.all(np.isfinite(traj1)) and int(st1["grad_evals"][0]) >= 1
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_largest_trajectory_against_oracle(k):
+    """N = 512, the largest trajectory the library accepts (DESIGN.md §8: the general kernel's LDS;
+    N = 513 is IRM_EINVAL, tests/test_abi.py): k GD steps on three problems against the oracle, inside
+    max(2·spread, ORACLE_FLOOR) as the bench-mode checks.  Only the first steps: at N = 512 the default
+    lr diverges (the oracle's loss goes 2.3-2.9 after one step to 10²-10³ after ten, its ±1-ulp spread
+    1e-3 → 0.1-0.6), so later steps would pin nothing."""
+    args = ("--optimizer-name", "gd", "--max-outer-iteration", 1, "--max-inner-iteration", k,
+            "--loop-loss-reduction", -1000000, "--n-timesteps", 512)
+    c = ctx(*args)
+    o = oracle_for(*args)
+    rng = np.random.default_rng(23)
+    B = 3
+    s = rng.uniform(-0.5, 0.5, (B, 3)).astype(np.float32)
+    g = rng.uniform(0.2, 1.6, (B, 3)).astype(np.float32)
+    obs = obstacles()
+    _, traj, st = c.optimize(s, g, obs)
+    assert traj.shape == (B, 512, 3) and np.all(st["grad_evals"] == k)
+    for b in range(B):
+        T, so, spread, lspread = _oracle_band(o, c.init_alpha(s[b], g[b]), obs, s[b], g[b], n_ens=4)
+        err = float(np.abs(traj[b] - T).max())
+        print(f"N=512 k={k} [{b}]: |traj - oracle| {err:.2e} (spread {spread:.2e}), "
+              f"loss {float(st['final_loss'][b]):.6f} vs {so['final_loss']:.6f}")
+        assert so["grad_evals"] == k
+        assert err <= max(2.0 * spread, ORACLE_FLOOR), (b, err, spread)
+        assert abs(float(st["final_loss"][b]) - so["final_loss"]) <= 1e-3 * abs(so["final_loss"]) + 3 * lspread
+
+
 def test_per_problem_obstacles_and_edge_counts():
     """obstacle_stride > 0: each problem its own obstacle set; also O = 0 and O = 64."""
     args = ("--optimizer-name", "gd", "--max-outer-iteration", 1, "--max-inner-iteration", 30)
